@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Benchmark of the nonce-search hot path (BASELINE.json metric: GH/s of the
+SHA-256 "msg nonce" min-search, and its fraction of the int32 VALU roofline).
+
+Workload = BASELINE config C2 (configs[1]): msg "bradfitz", nonces
+[0, 2^32-1] on one MI355X, bit-exact min (hash, nonce).  With --gpus N
+(torchrun, one process per GPU) the scaling is WEAK: rank r searches
+[r*2^32, (r+1)*2^32 - 1] on its own GPU, and the 16-byte partials are
+combined with one all_gather over RCCL (the only exchange the path has).
+
+A step = one complete search (all kernel launches, the second-pass
+reduction, the 16-byte result copy) of every rank's 2^32 nonces plus the
+combine.  value = total nonces of all ranks / max-over-ranks step time.
+
+Also reported:
+  roofline      dominant launch (the 10-digit segment) : algorithmic int32
+                ops (nonces x C x 1384) / its HIP-event time
+                on the library's stream, vs 78.64 T lane-ops/s per GPU.
+  cpu_baseline  the CPU oracle's loop shape (format + SHA-256 + strict '<',
+                OpenSSL block code) on this host's cores over a bounded
+                sample of the same workload (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+# torch first: libbtcminer.so then binds to torch's HIP runtime, so the
+# process holds exactly one (see tests/conftest.py).
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from distributed_bitcoin_minter_amd import Context  # noqa: E402
+from distributed_bitcoin_minter_amd.dist import combine  # noqa: E402
+
+MSG = b"bradfitz"
+PER_GPU = 1 << 32
+VALU_PEAK_T = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.64 T int32 lane-ops/s (MI355X_MICROARCH.md)
+OPS_PER_COMPRESSION = 1384                  # canonical int32 VALU ops
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def compressions_per_nonce(msg_len, digits):
+    """C(L, D) = ceil((L+D+10)/64) - floor((L+1)/64)."""
+    return -(-(msg_len + digits + 10) // 64) - (msg_len + 1) // 64
+
+
+def cpu_baseline(target_s=10.0):
+    """Time the oracle loop (test infrastructure: the CPU 'port' of
+    hash.go + miner.go) on this host over a bounded sample of C2."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from conftest import Oracle
+
+    path = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(path):
+        return None
+    oracle = Oracle(path)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    hi = PER_GPU - 1
+    n = 1 << 21
+    t = time.perf_counter()
+    oracle.search(MSG, hi - n + 1, hi, threads=threads, openssl=True)
+    rate = n / (time.perf_counter() - t)
+    n = int(min(PER_GPU, max(n, rate * target_s)))
+    t = time.perf_counter()
+    oracle.search(MSG, hi - n + 1, hi, threads=threads, openssl=True)
+    dt = time.perf_counter() - t
+    return {"value": n / dt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port",
+            "sample": f"msg 'bradfitz', last {n} nonces of [0, 2^32-1] (10-digit, 1 SHA-256 block each), "
+                      f"{threads} threads, snprintf-style format + OpenSSL SHA256 + strict '<' per nonce, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    lo = rank * PER_GPU
+    hi = lo + PER_GPU - 1
+    ctx = Context(devices=[local])
+    ctx.set_timing(True)
+
+    def step():
+        part = ctx.search(MSG, lo, hi)
+        dom = None
+        st = ctx.last_stats()
+        for i in range(st.recorded):
+            L = st.launch[i]
+            if dom is None or L.nonces > dom.nonces:
+                dom = L
+        res = combine(part, device=dev) if world > 1 else part
+        return res, (dom.nonces, dom.ms, dom.digits, dom.p, dom.grid, dom.tasks_per_thread, dom.inner_digits)
+
+    for _ in range(args.warmup):
+        res, _ = step()
+
+    def sync():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    sync()
+    t0 = time.perf_counter()
+    doms = []
+    for _ in range(args.steps):
+        res, d = step()
+        doms.append(d)
+    sync()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = tt.item()
+
+    total = PER_GPU * world * args.steps
+    value = total / dt / 1e9
+    dom_nonces, _, dom_digits, dom_p, dom_grid, dom_tpt, dom_inner = doms[-1]
+    dom_ms = sum(d[1] for d in doms) / len(doms)
+    C = compressions_per_nonce(len(MSG), dom_digits)
+    achieved = dom_nonces * C * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
+    check = None
+    if world == 1:
+        check = list(res)  # C2 golden: (5256245051, 1626825724)
+
+    out = {
+        "metric": "GH/s (SHA-256 \"msg nonce\" min-search) at 1/2/4/8 MI355X; % of int32 VALU peak",
+        "value": round(value, 4),
+        "unit": "GH/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": "C2: msg 'bradfitz', nonces [0, 2^32-1] per GPU (rank r: [r*2^32, (r+1)*2^32-1]), "
+                               "inclusive min (hash, nonce)",
+                   "msg": MSG.decode(), "nonces_per_gpu": PER_GPU, "global_nonces": PER_GPU * world,
+                   "parallelism": f"range-split x{world}" + (", RCCL all_gather of 16 B partials" if world > 1 else "")},
+        "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_T, 2),
+                     "unit": "T int32 lane-ops/s", "frac": round(achieved / VALU_PEAK_T, 4), "traffic": None,
+                     "kernel": f"search_kernel<P={dom_p},NBV=1> ({dom_digits}-digit nonces)",
+                     "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom_nonces,
+                     "ops_per_nonce": C * OPS_PER_COMPRESSION, "grid": dom_grid,
+                     "tasks_per_thread": dom_tpt, "inner_digits": dom_inner},
+        "result": check,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

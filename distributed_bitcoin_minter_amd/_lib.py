@@ -1,0 +1,197 @@
+"""ctypes binding of libbtcminer.so (C ABI: include/btcminer.h).
+
+The library is built in-tree (``make -C distributed_bitcoin_minter_amd/csrc``)
+and loaded from this package directory.  There is no fallback: if the
+library is missing, or there is no gfx950 device, calls raise.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbtcminer.so")
+
+BM_OK = 0
+BM_EINVAL = -1
+BM_ENODEV = -2
+BM_EHIP = -3
+BM_ERCCL = -4
+BM_ENOMEM = -5
+BM_EINTERNAL = -6
+BM_MAX_LAUNCH_STATS = 64
+U64_MAX = (1 << 64) - 1
+
+c_u64 = ctypes.c_uint64
+c_u32 = ctypes.c_uint32
+c_i32 = ctypes.c_int32
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("hash", c_u64), ("nonce", c_u64)]
+
+
+class LaunchStat(ctypes.Structure):
+    _fields_ = [("device", c_i32), ("p", c_i32), ("nbv", c_i32), ("pad_block", c_i32), ("digits", c_i32),
+                ("inner_digits", c_i32), ("nonces", c_u64), ("grid", c_u32), ("tasks_per_thread", c_u32),
+                ("ms", ctypes.c_double)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("launches", c_u32), ("recorded", c_u32), ("wall_ms", ctypes.c_double),
+                ("kernel_ms", ctypes.c_double), ("nonces", c_u64),
+                ("launch", LaunchStat * BM_MAX_LAUNCH_STATS)]
+
+
+class Segment(ctypes.Structure):
+    _fields_ = [("p", c_i32), ("nbv", c_i32), ("pad_block", c_i32), ("digits", c_i32), ("nd", c_i32),
+                ("max_inner", c_i32), ("vlo", c_u64), ("vhi", c_u64), ("nonce_base", c_u64),
+                ("mid", c_u32 * 8), ("tmpl", c_u32 * 32), ("pad_w", c_u32 * 16)]
+
+
+class BtcMinerError(RuntimeError):
+    def __init__(self, status, what):
+        self.status = status
+        super().__init__(f"{what}: {strerror(status)} ({status})")
+
+
+_lib = None
+
+
+def load():
+    """Load libbtcminer.so once; raises OSError if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} is missing: build it with `make -C {os.path.join(_HERE, 'csrc')} -j8` "
+                      "(or __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    vp = ctypes.c_void_p
+    sigs = {
+        "bm_abi_version": ([], ctypes.c_int),
+        "bm_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "bm_device_count": ([P(ctypes.c_int)], ctypes.c_int),
+        "bm_ctx_create": ([ctypes.c_int, P(vp)], ctypes.c_int),
+        "bm_ctx_create_devices": ([P(ctypes.c_int), ctypes.c_int, P(vp)], ctypes.c_int),
+        "bm_ctx_destroy": ([vp], ctypes.c_int),
+        "bm_ctx_num_devices": ([vp, P(ctypes.c_int)], ctypes.c_int),
+        "bm_search_gpu": ([vp, ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, P(Result)], ctypes.c_int),
+        "bm_hash_gpu": ([vp, ctypes.c_char_p, ctypes.c_size_t, P(c_u64), ctypes.c_size_t, P(c_u64)],
+                        ctypes.c_int),
+        "bm_ctx_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
+        "bm_ctx_last_stats": ([vp, P(Stats)], ctypes.c_int),
+        "bm_ctx_set_blocks_per_cu": ([vp, ctypes.c_int], ctypes.c_int),
+        "bm_ctx_set_max_windows": ([vp, ctypes.c_int], ctypes.c_int),
+        "bm_plan_segments": ([ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, P(Segment), ctypes.c_int,
+                              P(ctypes.c_int)], ctypes.c_int),
+        "bm_plan_segments_ex": ([ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, ctypes.c_int, P(Segment),
+                                 ctypes.c_int, P(ctypes.c_int)], ctypes.c_int),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def strerror(status):
+    try:
+        return load().bm_strerror(status).decode()
+    except OSError:
+        return f"status {status}"
+
+
+def check(status, what):
+    if status != BM_OK:
+        raise BtcMinerError(status, what)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(load().bm_device_count(ctypes.byref(n)), "bm_device_count")
+    return n.value
+
+
+DEFAULT_MAX_WINDOWS = 64
+
+
+def plan_segments(msg: bytes, lower: int, upper: int, max_windows: int = DEFAULT_MAX_WINDOWS):
+    """Host-side launch plan (pure CPU): list of Segment structs."""
+    lib = load()
+    n = ctypes.c_int(0)
+    f = lib.bm_plan_segments_ex
+    check(f(msg, len(msg), lower, upper, max_windows, None, 0, ctypes.byref(n)), "bm_plan_segments")
+    arr = (Segment * max(n.value, 1))()
+    check(f(msg, len(msg), lower, upper, max_windows, arr, n.value, ctypes.byref(n)), "bm_plan_segments")
+    return list(arr[: n.value])
+
+
+class Context:
+    """Owns a bm_ctx over one or more GPUs.  Not thread-safe (like the C ctx)."""
+
+    def __init__(self, devices=None, num_gpus=0):
+        lib = load()
+        h = ctypes.c_void_p()
+        if devices is not None:
+            ids = (ctypes.c_int * len(devices))(*devices)
+            check(lib.bm_ctx_create_devices(ids, len(devices), ctypes.byref(h)), "bm_ctx_create_devices")
+        else:
+            check(lib.bm_ctx_create(num_gpus, ctypes.byref(h)), "bm_ctx_create")
+        self._lib = lib
+        self._h = h
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise ValueError("context closed")
+        return self._h
+
+    def close(self):
+        if self._h is not None:
+            self._lib.bm_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def num_devices(self):
+        n = ctypes.c_int(0)
+        check(self._lib.bm_ctx_num_devices(self.handle, ctypes.byref(n)), "bm_ctx_num_devices")
+        return n.value
+
+    def search(self, msg: bytes, lower: int, upper: int):
+        """Inclusive [lower, upper] min-scan -> (hash, nonce)."""
+        r = Result()
+        check(self._lib.bm_search_gpu(self.handle, msg, len(msg), lower, upper, ctypes.byref(r)), "bm_search_gpu")
+        return r.hash, r.nonce
+
+    def hash_many(self, msg: bytes, nonces):
+        n = len(nonces)
+        arr = (c_u64 * max(n, 1))(*nonces)
+        out = (c_u64 * max(n, 1))()
+        check(self._lib.bm_hash_gpu(self.handle, msg, len(msg), arr, n, out), "bm_hash_gpu")
+        return list(out[:n])
+
+    def set_timing(self, on: bool):
+        check(self._lib.bm_ctx_set_timing(self.handle, 1 if on else 0), "bm_ctx_set_timing")
+
+    def set_max_windows(self, n: int):
+        check(self._lib.bm_ctx_set_max_windows(self.handle, n), "bm_ctx_set_max_windows")
+
+    def set_blocks_per_cu(self, n: int):
+        check(self._lib.bm_ctx_set_blocks_per_cu(self.handle, n), "bm_ctx_set_blocks_per_cu")
+
+    def last_stats(self):
+        s = Stats()
+        check(self._lib.bm_ctx_last_stats(self.handle, ctypes.byref(s)), "bm_ctx_last_stats")
+        return s

@@ -1,0 +1,493 @@
+// bm_api.hip -- C ABI of libbtcminer.so (include/btcminer.h): device
+// contexts, launch sizing, the per-device reduction and the multi-GPU
+// RCCL allgather of 16-byte partials.
+//
+// Drop-in for the reference miner's job loop body: miner.go:58-65 calls
+// bitcoin.Hash (hash.go:11-15) once per nonce and keeps a strict-'<' minimum;
+// bm_search_gpu returns the same (hash, nonce) for the same (msg, range).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "bm_aux_kernels.hpp"
+#include "bm_plan.hpp"
+#include "btcminer.h"
+
+namespace bm {
+
+// search kernel table [nbv-1][P], filled by bm_inst.hip at load time
+static const void* g_search[2][64];
+
+constexpr int kTasksPerThreadTarget = 16;  // balance: tasks per thread before growing S
+constexpr int kEventPairs = BM_MAX_LAUNCH_STATS;
+
+struct DeviceCtx {
+    int id = -1;
+    int cus = 0;
+    hipStream_t stream = nullptr;
+    Partial* d_part = nullptr;
+    size_t part_cap = 0;
+    Partial* d_result = nullptr;  // 1 partial
+    Partial* d_gather = nullptr;  // n_dev partials (allgather target)
+    Partial* h_result = nullptr;  // pinned, n_dev partials
+    uint64_t* d_hash_io = nullptr;
+    size_t hash_cap = 0;
+    hipEvent_t ev[2 * kEventPairs] = {};
+    ncclComm_t comm = nullptr;
+    std::vector<std::pair<const void*, int>> occ;  // kernel -> blocks per CU
+};
+
+struct Launch {
+    const void* fn;
+    SearchArgs args;
+    uint32_t grid;
+    bm_launch_stat_t stat;
+};
+
+namespace {
+int hip_status(hipError_t e) { return e == hipSuccess ? BM_OK : BM_EHIP; }
+
+#define BM_HIP(call)                                 \
+    do {                                             \
+        hipError_t e_ = (call);                      \
+        if (e_ != hipSuccess) return hip_status(e_); \
+    } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+}  // namespace bm
+
+struct bm_ctx {
+    std::vector<bm::DeviceCtx> devs;
+    bool timing = false;
+    int blocks_per_cu = 0;
+    int max_windows = bm::kDefaultMaxWindows;
+    bool nccl_ready = false;
+    bm_stats_t stats;
+};
+
+extern "C" void bm_register_search_kernel(int p, int nbv, const void* fn) {
+    if (p >= 0 && p < 64 && (nbv == 1 || nbv == 2)) bm::g_search[nbv - 1][p] = fn;
+}
+
+namespace bm {
+namespace {
+
+int blocks_per_cu(bm_ctx* ctx, DeviceCtx& d, const void* fn) {
+    if (ctx->blocks_per_cu > 0) return ctx->blocks_per_cu;
+    for (auto& e : d.occ)
+        if (e.first == fn) return e.second;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
+    d.occ.emplace_back(fn, nb);
+    return nb;
+}
+
+// Size one launch: S = 10^ms nonces per task, tasks spread evenly over a
+// grid that is fully resident (grid-stride, every thread the same count
+// +-1), so the launch drains together.
+int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_off, Launch& L) {
+    const void* fn = g_search[s.nbv - 1][s.p];
+    if (!fn) return BM_EINTERNAL;
+    const uint64_t gmax = (uint64_t)blocks_per_cu(ctx, d, fn) * (uint64_t)d.cus * kBlock;
+    int ms = 1;
+    for (int m = s.max_inner; m >= 1; --m) {
+        const uint64_t S = kPow10[m];
+        const uint64_t T = s.vhi / S - s.vlo / S + 1;
+        if (T >= (uint64_t)kTasksPerThreadTarget * gmax) {
+            ms = m;
+            break;
+        }
+    }
+    const uint64_t S = kPow10[ms];
+    const uint64_t t0 = s.vlo / S, t_end = s.vhi / S + 1;
+    const uint64_t T = t_end - t0;
+    const uint64_t k = (T + gmax - 1) / gmax;       // tasks per thread
+    const uint64_t G = (T + k - 1) / k;             // threads needed
+    const uint64_t grid = (G + kBlock - 1) / kBlock;
+    if (grid == 0 || grid > 0x7fffffffull) return BM_EINTERNAL;
+
+    SearchArgs& A = L.args;
+    std::memset(&A, 0, sizeof A);
+    std::memcpy(A.mid, s.mid, sizeof A.mid);
+    std::memcpy(A.tmpl, s.tmpl, sizeof A.tmpl);
+    if (s.pad_block) {
+        uint32_t w[64];
+        for (int i = 0; i < 16; ++i) w[i] = s.pad_w[i];
+        host::expand(w);
+        for (int i = 0; i < 64; ++i) A.padkw[i] = kK256[i] + w[i];
+    }
+    A.vlo = s.vlo;
+    A.vhi = s.vhi;
+    A.nonce_base = s.nonce_base;
+    A.t0 = t0;
+    A.t_end = t_end;
+    A.stride = grid * kBlock;
+    A.S = (uint32_t)S;
+    A.ms = (uint32_t)ms;
+    A.nd = (uint32_t)s.nd;
+    A.part_off = part_off;
+    L.fn = fn;
+    L.grid = (uint32_t)grid;
+    std::memset(&L.stat, 0, sizeof L.stat);
+    L.stat.p = s.p;
+    L.stat.nbv = s.nbv;
+    L.stat.pad_block = s.pad_block;
+    L.stat.digits = s.digits;
+    L.stat.inner_digits = ms;
+    L.stat.nonces = s.vhi - s.vlo + 1;
+    L.stat.grid = (uint32_t)grid;
+    L.stat.tasks_per_thread = (uint32_t)k;
+    return BM_OK;
+}
+
+int ensure_partials(DeviceCtx& d, size_t n) {
+    if (n <= d.part_cap) return BM_OK;
+    if (d.d_part) BM_HIP(hipFree(d.d_part));
+    d.d_part = nullptr;
+    d.part_cap = 0;
+    size_t cap = std::max<size_t>(n, 4096);
+    BM_HIP(hipMalloc(&d.d_part, cap * sizeof(Partial)));
+    d.part_cap = cap;
+    return BM_OK;
+}
+
+int init_device(DeviceCtx& d, int id, int ndev) {
+    d.id = id;
+    BM_HIP(hipSetDevice(id));
+    hipDeviceProp_t prop;
+    BM_HIP(hipGetDeviceProperties(&prop, id));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return BM_ENODEV;  // kernels are gfx950 code objects
+    d.cus = prop.multiProcessorCount;
+    BM_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    BM_HIP(hipMalloc(&d.d_result, sizeof(Partial)));
+    BM_HIP(hipMalloc(&d.d_gather, sizeof(Partial) * (size_t)ndev));
+    BM_HIP(hipHostMalloc(&d.h_result, sizeof(Partial) * (size_t)ndev, hipHostMallocDefault));
+    for (auto& e : d.ev) BM_HIP(hipEventCreate(&e));
+    return ensure_partials(d, 4096);
+}
+
+void destroy_device(DeviceCtx& d) {
+    if (d.id < 0) return;
+    (void)hipSetDevice(d.id);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    if (d.comm) (void)ncclCommDestroy(d.comm);
+    for (auto& e : d.ev)
+        if (e) (void)hipEventDestroy(e);
+    if (d.d_part) (void)hipFree(d.d_part);
+    if (d.d_result) (void)hipFree(d.d_result);
+    if (d.d_gather) (void)hipFree(d.d_gather);
+    if (d.d_hash_io) (void)hipFree(d.d_hash_io);
+    if (d.h_result) (void)hipHostFree(d.h_result);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+}
+
+int ensure_nccl(bm_ctx* ctx) {
+    if (ctx->nccl_ready || ctx->devs.size() < 2) return BM_OK;
+    const int n = (int)ctx->devs.size();
+    std::vector<ncclComm_t> comms(n);
+    std::vector<int> ids(n);
+    for (int i = 0; i < n; ++i) ids[i] = ctx->devs[i].id;
+    if (ncclCommInitAll(comms.data(), n, ids.data()) != ncclSuccess) return BM_ERCCL;
+    for (int i = 0; i < n; ++i) ctx->devs[i].comm = comms[i];
+    ctx->nccl_ready = true;
+    return BM_OK;
+}
+
+int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, bm_result_t* out) {
+    const auto t_start = std::chrono::steady_clock::now();
+    bm_stats_t& st = ctx->stats;
+    std::memset(&st, 0, sizeof st);
+    const int ndev = (int)ctx->devs.size();
+    if (lower > upper) {  // miner.go:45-46 with zero iterations
+        out->hash = UINT64_MAX;
+        out->nonce = UINT64_MAX;
+        return BM_OK;
+    }
+    st.nonces = upper - lower + 1;  // wraps to 0 only for the full 2^64 range
+
+    // 1. split the range over devices, plan and size every launch
+    const std::vector<Piece> pieces = split_range(lower, upper, ndev);
+    std::vector<std::vector<Launch>> launches(ndev);
+    for (int di = 0; di < ndev; ++di) {
+        if (di >= (int)pieces.size()) continue;
+        std::vector<bm_segment_t> segs;
+        int rc = plan_segments(msg, len, pieces[di].lo, pieces[di].hi, segs, ctx->max_windows);
+        if (rc != BM_OK) return rc;
+        uint32_t off = 0;
+        for (const auto& s : segs) {
+            Launch L;
+            rc = size_launch(ctx, ctx->devs[di], s, off, L);
+            if (rc != BM_OK) return rc;
+            L.stat.device = di;
+            off += L.grid;
+            launches[di].push_back(L);
+        }
+        BM_HIP(hipSetDevice(ctx->devs[di].id));
+        rc = ensure_partials(ctx->devs[di], off);
+        if (rc != BM_OK) return rc;
+    }
+
+    // 2. enqueue: search launches, then the second-pass reduction
+    for (int di = 0; di < ndev; ++di) {
+        DeviceCtx& d = ctx->devs[di];
+        BM_HIP(hipSetDevice(d.id));
+        uint32_t nparts = 0, li = 0;
+        for (Launch& L : launches[di]) {
+            const bool timed = ctx->timing && li < (uint32_t)kEventPairs;
+            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li], d.stream));
+            void* kargs[] = {&L.args, &d.d_part};
+            BM_HIP(hipLaunchKernel(L.fn, dim3(L.grid), dim3(kBlock), kargs, 0, d.stream));
+            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li + 1], d.stream));
+            nparts += L.grid;
+            ++li;
+        }
+        reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, d.d_result);
+        BM_HIP(hipGetLastError());
+    }
+
+    // 3. combine: one RCCL allgather of the 16-byte partials, or a plain copy
+    if (ndev > 1) {
+        int rc = ensure_nccl(ctx);
+        if (rc != BM_OK) return rc;
+        if (ncclGroupStart() != ncclSuccess) return BM_ERCCL;
+        for (int di = 0; di < ndev; ++di) {
+            DeviceCtx& d = ctx->devs[di];
+            if (ncclAllGather(d.d_result, d.d_gather, 2, ncclUint64, d.comm, d.stream) != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return BM_ERCCL;
+            }
+        }
+        if (ncclGroupEnd() != ncclSuccess) return BM_ERCCL;
+        DeviceCtx& d0 = ctx->devs[0];
+        BM_HIP(hipSetDevice(d0.id));
+        BM_HIP(hipMemcpyAsync(d0.h_result, d0.d_gather, sizeof(Partial) * ndev, hipMemcpyDeviceToHost, d0.stream));
+    } else {
+        DeviceCtx& d0 = ctx->devs[0];
+        BM_HIP(hipMemcpyAsync(d0.h_result, d0.d_result, sizeof(Partial), hipMemcpyDeviceToHost, d0.stream));
+    }
+    for (int di = 0; di < ndev; ++di) {
+        BM_HIP(hipSetDevice(ctx->devs[di].id));
+        BM_HIP(hipStreamSynchronize(ctx->devs[di].stream));
+    }
+
+    Partial best{UINT64_MAX, UINT64_MAX};
+    for (int di = 0; di < ndev; ++di) {
+        const Partial& p = ctx->devs[0].h_result[di];
+        if (p.hash < best.hash || (p.hash == best.hash && p.nonce < best.nonce)) best = p;
+    }
+
+    // 4. statistics
+    for (int di = 0; di < ndev; ++di) {
+        DeviceCtx& d = ctx->devs[di];
+        uint32_t li = 0;
+        for (Launch& L : launches[di]) {
+            ++st.launches;
+            if (ctx->timing && li < (uint32_t)kEventPairs) {
+                float ms = 0.f;
+                BM_HIP(hipEventElapsedTime(&ms, d.ev[2 * li], d.ev[2 * li + 1]));
+                L.stat.ms = ms;
+                st.kernel_ms += ms;
+            }
+            if (st.recorded < BM_MAX_LAUNCH_STATS) st.launch[st.recorded++] = L.stat;
+            ++li;
+        }
+    }
+    st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    out->hash = best.hash;
+    out->nonce = best.nonce;
+    return BM_OK;
+}
+
+int hash_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, const uint64_t* nonces, size_t n, uint64_t* out) {
+    if (n == 0) return BM_OK;
+    DeviceCtx& d = ctx->devs[0];
+    BM_HIP(hipSetDevice(d.id));
+    HashArgs A;
+    std::memset(&A, 0, sizeof A);
+    // midstate over the whole 64-byte blocks of "msg "
+    const uint64_t pre = (uint64_t)len + 1;
+    const uint64_t full = pre / 64;
+    uint32_t st[8];
+    for (int i = 0; i < 8; ++i) st[i] = kIV256[i];
+    uint8_t blk[64];
+    for (uint64_t b = 0; b < full; ++b) {
+        for (int i = 0; i < 64; ++i) {
+            const uint64_t pos = b * 64 + (uint64_t)i;
+            blk[i] = pos < len ? msg[pos] : (uint8_t)' ';
+        }
+        host::compress_bytes(st, blk);
+    }
+    std::memcpy(A.mid, st, sizeof st);
+    A.tail_len = (uint32_t)(pre - full * 64);
+    for (uint32_t i = 0; i < A.tail_len; ++i) {
+        const uint64_t pos = full * 64 + i;
+        A.tail[i] = pos < len ? msg[pos] : (uint8_t)' ';
+    }
+    A.total_prefix = pre;
+    A.n = n;
+    if (n > d.hash_cap) {
+        if (d.d_hash_io) BM_HIP(hipFree(d.d_hash_io));
+        d.d_hash_io = nullptr;
+        d.hash_cap = 0;
+        BM_HIP(hipMalloc(&d.d_hash_io, 2 * n * sizeof(uint64_t)));
+        d.hash_cap = n;
+    }
+    BM_HIP(hipMemcpyAsync(d.d_hash_io, nonces, n * sizeof(uint64_t), hipMemcpyHostToDevice, d.stream));
+    const uint64_t grid = (n + kHashThreads - 1) / kHashThreads;
+    hash_kernel<<<dim3((uint32_t)grid), kHashThreads, 0, d.stream>>>(A, d.d_hash_io, d.d_hash_io + n);
+    BM_HIP(hipGetLastError());
+    BM_HIP(hipMemcpyAsync(out, d.d_hash_io + n, n * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+    BM_HIP(hipStreamSynchronize(d.stream));
+    return BM_OK;
+}
+
+}  // namespace
+}  // namespace bm
+
+// ------------------------------------------------------------------ C ABI --
+
+extern "C" {
+
+int bm_abi_version(void) { return BM_ABI_VERSION; }
+
+const char* bm_strerror(int status) {
+    switch (status) {
+        case BM_OK: return "ok";
+        case BM_EINVAL: return "invalid argument";
+        case BM_ENODEV: return "no usable gfx950 device";
+        case BM_EHIP: return "HIP runtime error";
+        case BM_ERCCL: return "RCCL error";
+        case BM_ENOMEM: return "out of memory";
+        case BM_EINTERNAL: return "internal error";
+        default: return "unknown status";
+    }
+}
+
+int bm_device_count(int* out) {
+    if (!out) return BM_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return BM_OK;
+}
+
+int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out) {
+    if (!out || !devices || n < 1) return BM_EINVAL;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1) return BM_ENODEV;
+    for (int i = 0; i < n; ++i)
+        if (devices[i] < 0 || devices[i] >= count) return BM_ENODEV;
+    bm_ctx* ctx = new (std::nothrow) bm_ctx();
+    if (!ctx) return BM_ENOMEM;
+    std::memset(&ctx->stats, 0, sizeof ctx->stats);
+    bm::DeviceGuard guard;
+    ctx->devs.resize(n);
+    for (int i = 0; i < n; ++i) {
+        int rc = bm::init_device(ctx->devs[i], devices[i], n);
+        if (rc != BM_OK) {
+            for (auto& d : ctx->devs) bm::destroy_device(d);
+            delete ctx;
+            return rc;
+        }
+    }
+    *out = ctx;
+    return BM_OK;
+}
+
+int bm_ctx_create(int num_gpus, bm_ctx_t** out) {
+    if (!out || num_gpus < 0) return BM_EINVAL;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1) return BM_ENODEV;
+    if (num_gpus == 0) num_gpus = count;
+    if (num_gpus > count) return BM_ENODEV;
+    std::vector<int> ids(num_gpus);
+    for (int i = 0; i < num_gpus; ++i) ids[i] = i;
+    return bm_ctx_create_devices(ids.data(), num_gpus, out);
+}
+
+int bm_ctx_destroy(bm_ctx_t* ctx) {
+    if (!ctx) return BM_EINVAL;
+    bm::DeviceGuard guard;
+    for (auto& d : ctx->devs) bm::destroy_device(d);
+    delete ctx;
+    return BM_OK;
+}
+
+int bm_ctx_num_devices(const bm_ctx_t* ctx, int* out) {
+    if (!ctx || !out) return BM_EINVAL;
+    *out = (int)ctx->devs.size();
+    return BM_OK;
+}
+
+int bm_search_gpu(bm_ctx_t* ctx, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, bm_result_t* out) {
+    if (!ctx || !out || (len && !msg) || len > BM_MAX_MSG_LEN) return BM_EINVAL;
+    bm::DeviceGuard guard;
+    bm_result_t r;
+    int rc = bm::search_impl(ctx, msg, len, lower, upper, &r);
+    if (rc == BM_OK) *out = r;
+    return rc;
+}
+
+int bm_hash_gpu(bm_ctx_t* ctx, const uint8_t* msg, size_t len, const uint64_t* nonces, size_t n, uint64_t* out) {
+    if (!ctx || (n && (!nonces || !out)) || (len && !msg) || len > BM_MAX_MSG_LEN) return BM_EINVAL;
+    bm::DeviceGuard guard;
+    return bm::hash_impl(ctx, msg, len, nonces, n, out);
+}
+
+int bm_ctx_set_timing(bm_ctx_t* ctx, int enable) {
+    if (!ctx) return BM_EINVAL;
+    ctx->timing = enable != 0;
+    return BM_OK;
+}
+
+int bm_ctx_last_stats(const bm_ctx_t* ctx, bm_stats_t* out) {
+    if (!ctx || !out) return BM_EINVAL;
+    *out = ctx->stats;
+    return BM_OK;
+}
+
+int bm_ctx_set_blocks_per_cu(bm_ctx_t* ctx, int blocks_per_cu) {
+    if (!ctx || blocks_per_cu < 0 || blocks_per_cu > 32) return BM_EINVAL;
+    ctx->blocks_per_cu = blocks_per_cu;
+    return BM_OK;
+}
+
+int bm_ctx_set_max_windows(bm_ctx_t* ctx, int max_windows) {
+    if (!ctx || max_windows < 0) return BM_EINVAL;
+    ctx->max_windows = max_windows;
+    return BM_OK;
+}
+
+int bm_plan_segments(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, bm_segment_t* segs, int cap,
+                     int* nseg) {
+    return bm_plan_segments_ex(msg, len, lower, upper, bm::kDefaultMaxWindows, segs, cap, nseg);
+}
+
+int bm_plan_segments_ex(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, int max_windows,
+                        bm_segment_t* segs, int cap, int* nseg) {
+    if (!nseg || cap < 0 || (cap > 0 && !segs)) return BM_EINVAL;
+    std::vector<bm_segment_t> v;
+    int rc = bm::plan_segments(msg, len, lower, upper, v, max_windows);
+    if (rc != BM_OK) return rc;
+    *nseg = (int)v.size();
+    for (int i = 0; i < cap && i < (int)v.size(); ++i) segs[i] = v[i];
+    return BM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,26 @@
+// bm_inst.hip -- explicit instantiations of search_kernel<P, NBV> for
+// P in [BM_INST_PLO, BM_INST_PHI] and NBV = BM_INST_NBV, registered into the
+// launcher's table at load time.  The Makefile compiles this file once per
+// P range (in parallel) so a full build of all 83 layouts stays short.
+#include "bm_kernels.hpp"
+
+#if !defined(BM_INST_PLO) || !defined(BM_INST_PHI) || !defined(BM_INST_NBV)
+#error "define BM_INST_PLO, BM_INST_PHI and BM_INST_NBV"
+#endif
+
+extern "C" void bm_register_search_kernel(int p, int nbv, const void* fn);
+
+#include <utility>
+
+namespace {
+template <int... I>
+void register_all(std::integer_sequence<int, I...>) {
+    (bm_register_search_kernel(BM_INST_PLO + I, BM_INST_NBV,
+                               reinterpret_cast<const void*>(&bm::search_kernel<BM_INST_PLO + I, BM_INST_NBV>)),
+     ...);
+}
+struct Registrar {
+    Registrar() { register_all(std::make_integer_sequence<int, BM_INST_PHI - BM_INST_PLO + 1>{}); }
+};
+const Registrar registrar;
+}  // namespace

@@ -1,0 +1,337 @@
+// bm_kernels.hpp -- gfx950 (CDNA4) kernels for the nonce search.
+//
+// Replaces the reference's per-nonce bitcoin.Hash call inside the miner's
+// min-scan (/root/reference/project2/bitcoin/hash.go:11-15 and
+// bitcoin/miner/miner.go:58-65) with one integer-VALU-bound kernel:
+//
+//   * Each lane owns a "task": S = 10^ms consecutive values of v whose
+//     high digits (the task index t) are constant.  The task's digits are
+//     formatted once per task (64-bit divide-by-10 chain) and added into the
+//     template words.
+//   * The ms low digits sit in ONE 32-bit message word (word LW of the last
+//     block) and are identical in all 64 lanes at every inner iteration, so
+//     they are kept in SGPRs and stepped on the scalar unit.
+//   * Rounds 0..LW-1 of the last block depend only on task-constant words and
+//     are computed once per task; the schedule terms that do not depend on
+//     word LW are loop-invariant and hoisted out of the inner loop.
+//   * Words after LW are compile-time constants (zeros / the 0x80 pad byte),
+//     so the schedule sheds their terms at compile time (template P = byte
+//     position of the last digit).
+//   * Rotations are v_alignbit_b32, Sigma/sigma xors and Ch/Maj are single
+//     v_bitop3_b32 (gfx950), sums fold into v_add3_u32.
+//   * The running minimum is compared on the first state word only; the
+//     exact 64-bit compare, the range check and the update run on the rare
+//     path (a new low is seen ~ln(n) times per lane).
+//   * Ties: a lane scans its nonces in ascending order with a strict '<', and
+//     every reduction above it is a lexicographic (hash, nonce) min, which
+//     equals the reference's sequential strict-'<' scan.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "bm_common.h"
+#include "bm_sha256.hpp"
+
+namespace bm {
+
+#define BM_DEV __device__ __forceinline__
+
+template <int B, int E, class F>
+BM_DEV void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+BM_DEV uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+// 3-input bitwise ops as one v_bitop3_b32; constant operands fold in C instead
+// (the intrinsic is opaque to constant folding).
+BM_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    if (__builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c)) return a ^ b ^ c;
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+BM_DEV uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+    if (__builtin_constant_p(e) && __builtin_constant_p(f) && __builtin_constant_p(g)) return (e & f) ^ (~e & g);
+    return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+BM_DEV uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+    if (__builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c))
+        return (a & b) ^ (a & c) ^ (b & c);
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+BM_DEV uint32_t bsig0(uint32_t a) { return xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)); }
+BM_DEV uint32_t bsig1(uint32_t e) { return xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)); }
+BM_DEV uint32_t ssig0(uint32_t x) { return xor3(rotr(x, 7), rotr(x, 18), x >> 3); }
+BM_DEV uint32_t ssig1(uint32_t x) { return xor3(rotr(x, 17), rotr(x, 19), x >> 10); }
+
+// Round T on a rotating register file: entering round T, role r (a=0..h=7)
+// lives in s[(r - T) & 7], so no values move between rounds.
+template <int T>
+BM_DEV void sha_round(uint32_t (&s)[8], uint32_t w) {
+    uint32_t& a = s[(0 - T) & 7];
+    uint32_t& b = s[(1 - T) & 7];
+    uint32_t& c = s[(2 - T) & 7];
+    uint32_t& d = s[(3 - T) & 7];
+    uint32_t& e = s[(4 - T) & 7];
+    uint32_t& f = s[(5 - T) & 7];
+    uint32_t& g = s[(6 - T) & 7];
+    uint32_t& h = s[(7 - T) & 7];
+    const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + (kK256[T] + w);
+    d += t1;
+    h = t1 + bsig0(a) + maj(a, b, c);
+}
+
+// Same round with K[T] + W[T] supplied pre-added (constant padding block).
+template <int T>
+BM_DEV void sha_round_kw(uint32_t (&s)[8], uint32_t kw) {
+    uint32_t& a = s[(0 - T) & 7];
+    uint32_t& b = s[(1 - T) & 7];
+    uint32_t& c = s[(2 - T) & 7];
+    uint32_t& d = s[(3 - T) & 7];
+    uint32_t& e = s[(4 - T) & 7];
+    uint32_t& f = s[(5 - T) & 7];
+    uint32_t& g = s[(6 - T) & 7];
+    uint32_t& h = s[(7 - T) & 7];
+    const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw;
+    d += t1;
+    h = t1 + bsig0(a) + maj(a, b, c);
+}
+
+// Rounds [R0, R1) of one block; w is the 16-word schedule window holding
+// W[t] at w[t & 15] (the raw block words on entry when R0 <= 16).
+template <int R0, int R1>
+BM_DEV void sha_rounds(uint32_t (&s)[8], uint32_t (&w)[16]) {
+    static_for<R0, R1>([&](auto I) {
+        constexpr int t = decltype(I)::value;
+        if constexpr (t >= 16)
+            w[t & 15] = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
+        sha_round<t>(s, w[t & 15]);
+    });
+}
+
+// Full compression: st = st + F(st, block).
+BM_DEV void sha_compress(uint32_t (&st)[8], uint32_t (&w)[16]) {
+    uint32_t s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = st[i];
+    sha_rounds<0, 64>(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] += s[i];
+}
+
+// Compile-time value of last-block word k > LW, or -1 when it is runtime
+// (the bit-length word of a non-padding layout).
+template <int P, bool PADB>
+constexpr int64_t tail_word(int k) {
+    constexpr int LW = P / 4;
+    if (k == LW + 1 && (P % 4) == 3 && P != 63) return 0x80000000ll;  // 0x80 spilled into the next word
+    if (!PADB && k == 15) return -1;  // 8 * message length
+    return 0;                         // zeros (and word 14: length < 2^32 bits)
+}
+
+// Add the digits of task t into the words: v's digit i (0 = least
+// significant) lives at byte 64*(NBV-1) + P - i of the varying region.
+// Digits i in [ms, nd) come from t; digits below ms are the inner loop's.
+template <int P, int NBV>
+BM_DEV void add_task_digits(uint32_t (&W)[16 * NBV], uint64_t t, uint32_t ms, uint32_t nd) {
+    uint64_t x = t;
+    static_for<1, 20>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        constexpr int pos = 64 * (NBV - 1) + P - i;
+        if constexpr (pos >= 0) {
+            if (i >= (int)ms && i < (int)nd) {  // wave-uniform
+                const uint64_t q = x / 10u;
+                const uint32_t d = (uint32_t)(x - q * 10u);
+                x = q;
+                W[pos >> 2] += d << (8 * (3 - (pos & 3)));
+            }
+        }
+    });
+}
+
+// Lexicographic (hash, nonce) compare.
+BM_DEV bool lex_less(uint64_t h1, uint64_t n1, uint64_t h2, uint64_t n2) {
+    return h1 < h2 || (h1 == h2 && n1 < n2);
+}
+
+template <int XOR>
+BM_DEV uint64_t swizzle_xor_u64(uint64_t v) {
+    // ds_swizzle bitmask mode: lane' = lane ^ XOR within each 32-lane half
+    constexpr int pat = (XOR << 10) | 0x1F;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)v, pat);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(v >> 32), pat);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+BM_DEV uint64_t readlane_u64(uint64_t v, int lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Wave-wide lexicographic min: ds_swizzle xor butterflies inside each 32-lane
+// half, then the two halves via readlane.  Result valid in every lane.
+BM_DEV void wave_min(uint64_t& h, uint64_t& n) {
+    static_for<0, 5>([&](auto I) {
+        constexpr int x = 1 << decltype(I)::value;
+        const uint64_t oh = swizzle_xor_u64<x>(h), on = swizzle_xor_u64<x>(n);
+        if (lex_less(oh, on, h, n)) {
+            h = oh;
+            n = on;
+        }
+    });
+    const uint64_t h0 = readlane_u64(h, 0), n0 = readlane_u64(n, 0);
+    const uint64_t h1 = readlane_u64(h, 32), n1 = readlane_u64(n, 32);
+    if (lex_less(h1, n1, h0, n0)) {
+        h = h1;
+        n = n1;
+    } else {
+        h = h0;
+        n = n0;
+    }
+}
+
+// Workgroup min of (h, n) -> thread 0 returns true with the result.
+template <int NT>
+BM_DEV bool block_min(uint64_t& h, uint64_t& n) {
+    constexpr int NWAVE = NT / 64;
+    __shared__ Partial sh[NWAVE];
+    wave_min(h, n);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sh[wave] = Partial{h, n};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 1; i < NWAVE; ++i)
+            if (lex_less(sh[i].hash, sh[i].nonce, h, n)) {
+                h = sh[i].hash;
+                n = sh[i].nonce;
+            }
+        return true;
+    }
+    return false;
+}
+
+// The search kernel for one layout.  P = byte index (0..63) of the last
+// digit inside the last varying block; NBV = 2 when each task also
+// re-compresses the block before it (high digits there).
+template <int P, int NBV>
+__global__ __launch_bounds__(kBlock) void search_kernel(const SearchArgs A, Partial* __restrict__ part) {
+    static_assert(P >= 0 && P < 64 && (NBV == 1 || (NBV == 2 && P <= 18)), "layout");
+    constexpr int LW = P / 4;                      // last-block word holding the last digit
+    constexpr int BOFF = 16 * (NBV - 1);           // word offset of the last block
+    constexpr bool PADB = (NBV == 1) && (P >= 55); // a constant padding block follows
+
+    // Inner-loop digit steps: digit i (< ms) of the inner counter sits at
+    // bit 8*(3 - P%4 + i) of word LW.
+    constexpr uint32_t inc0 = 1u << (8 * (3 - P % 4));
+    constexpr uint32_t inc1 = (P % 4) >= 1 ? 1u << (8 * (4 - P % 4)) : 0u;
+    constexpr uint32_t inc2 = (P % 4) >= 2 ? 1u << (8 * (5 - P % 4)) : 0u;
+    constexpr uint32_t inc3 = (P % 4) >= 3 ? 1u << (8 * (6 - P % 4)) : 0u;
+
+    uint64_t best_h = ~0ull, best_n = ~0ull;
+    uint32_t bh = 0xFFFFFFFFu;  // high word of best_h
+
+    const uint32_t S = A.S;
+    for (uint64_t t = A.t0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < A.t_end; t += A.stride) {
+        // ---- per task: words, block before (NBV=2), rounds 0..LW-1 ----
+        uint32_t W[16 * NBV];
+        static_for<0, 16 * NBV>([&](auto K) { W[decltype(K)::value] = A.tmpl[decltype(K)::value]; });
+        add_task_digits<P, NBV>(W, t, A.ms, A.nd);
+
+        uint32_t st[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st[i] = A.mid[i];
+        if constexpr (NBV == 2) {
+            uint32_t wa[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) wa[k] = W[k];
+            sha_compress(st, wa);
+        }
+
+        uint32_t wb[16];
+        static_for<0, 16>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            if constexpr (k <= LW) {
+                wb[k] = W[BOFF + k];
+            } else {
+                constexpr int64_t c = tail_word<P, PADB>(k);
+                if constexpr (c < 0)
+                    wb[k] = A.tmpl[BOFF + k];
+                else
+                    wb[k] = (uint32_t)c;
+            }
+        });
+        uint32_t s0[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s0[i] = st[i];
+        sha_rounds<0, LW>(s0, wb);
+        const uint32_t wl = wb[LW];
+
+        // ---- inner loop over the ms uniform low digits ----
+        const uint64_t vbase = t * (uint64_t)S;
+        uint32_t J = 0, c0 = 0, c1 = 0, c2 = 0;
+        for (uint32_t j = 0; j < S; ++j) {
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = wb[k];
+            w[LW] = wl + J;
+            uint32_t x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = s0[i];
+            sha_rounds<LW, 64>(x, w);
+
+            uint32_t h0, h1;
+            if constexpr (PADB) {
+                uint32_t y[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) y[i] = st[i] + x[i];
+                uint32_t z[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) z[i] = y[i];
+                static_for<0, 64>([&](auto I) {
+                    constexpr int tt = decltype(I)::value;
+                    sha_round_kw<tt>(z, A.padkw[tt]);
+                });
+                h0 = y[0] + z[0];
+                h1 = y[1] + z[1];
+            } else {
+                h0 = st[0] + x[0];
+                h1 = st[1] + x[1];
+            }
+
+            if (__builtin_expect(h0 <= bh, 0)) {
+                const uint64_t h = ((uint64_t)h0 << 32) | h1;
+                const uint64_t v = vbase + j;
+                if (h < best_h && v >= A.vlo && v <= A.vhi) {
+                    best_h = h;
+                    best_n = A.nonce_base + v;
+                    bh = h0;
+                }
+            }
+
+            // step the uniform decimal counter held in word LW
+            J += inc0;
+            if (++c0 == 10u) {
+                c0 = 0;
+                J += inc1 - 10u * inc0;
+                if (++c1 == 10u) {
+                    c1 = 0;
+                    J += inc2 - 10u * inc1;
+                    if (++c2 == 10u) {
+                        c2 = 0;
+                        J += inc3 - 10u * inc2;
+                    }
+                }
+            }
+        }
+    }
+
+    if (block_min<kBlock>(best_h, best_n)) part[A.part_off + blockIdx.x] = Partial{best_h, best_n};
+}
+
+}  // namespace bm

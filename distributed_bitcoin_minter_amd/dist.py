@@ -1,0 +1,65 @@
+"""Multi-process (one process per GPU) sharding of a nonce search.
+
+The nonce range shards with no data exchange: rank r scans its contiguous
+piece of [lower, upper] on its own GPU, and the only collective is one
+all_gather of the 16-byte partial {hash, nonce} per rank, followed by a
+lexicographic (hash, nonce) min, which equals the reference's sequential
+strict-'<' scan (miner.go:59-65).  Inside one process the
+same split is done by a multi-device bm_ctx with an RCCL allgather
+(csrc/bm_api.hip).  With torch.distributed's "nccl" backend (RCCL on ROCm)
+the gather runs over xGMI; "gloo" is used for CPU tests.
+"""
+U64_MAX = (1 << 64) - 1
+
+
+def split_range(lower: int, upper: int, n: int):
+    """Contiguous near-equal inclusive pieces; mirrors bm::split_range
+    (csrc/bm_plan.cpp).  Returns at most n pieces (fewer for short ranges)."""
+    if lower > upper or n < 1:
+        return []
+    span = upper - lower
+    n = min(n, span + 1)
+    q, r = divmod(span, n)
+    out, cur = [], lower
+    for i in range(n):
+        size_m1 = q if i <= r else q - 1
+        out.append((cur, cur + size_m1))
+        cur = cur + size_m1 + 1
+    out[-1] = (out[-1][0], upper)
+    return out
+
+
+def lex_min(pairs):
+    """Lexicographic (hash, nonce) min; (2^64-1, 2^64-1) for no pairs."""
+    best = (U64_MAX, U64_MAX)
+    for p in pairs:
+        if tuple(p) < best:
+            best = tuple(p)
+    return best
+
+
+def rank_piece(lower: int, upper: int, rank: int, world: int):
+    """This rank's inclusive piece, or None if the range is shorter than world."""
+    pieces = split_range(lower, upper, world)
+    return pieces[rank] if rank < len(pieces) else None
+
+
+def combine(partial, device=None):
+    """All-gather every rank's (hash, nonce) and return the global min.
+
+    One collective of 2 x uint64 per rank: dist.all_gather_into_tensor on a
+    uint64 tensor (RCCL when the process group is "nccl")."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size()
+    h, n = partial
+    # two's-complement view: uint64 -> int64 bits survive the exchange
+    def s64(x):
+        return x - (1 << 64) if x >= 1 << 63 else x
+
+    src = torch.tensor([s64(h), s64(n)], dtype=torch.int64, device=device)
+    dst = torch.empty(2 * world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(dst, src)
+    vals = [v & U64_MAX for v in dst.cpu().tolist()]
+    return lex_min((vals[2 * i], vals[2 * i + 1]) for i in range(world))

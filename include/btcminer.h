@@ -1,0 +1,162 @@
+/*
+ * btcminer.h -- C ABI of libbtcminer.so, the MI355X (gfx950) nonce-search
+ * backend for the distributed bitcoin miner.
+ *
+ * What it replaces in the reference (/root/reference/project2):
+ *   bitcoin.Hash(msg string, nonce uint64) uint64          bitcoin/hash.go:11-15
+ *   the miner's min-scan over a job's nonce range          bitcoin/miner/miner.go:43-74
+ *                                                           (init :45-46, hot loop :58-65)
+ * The Go miner would bind these with cgo; everything
+ * else in the reference (LSP transport, JSON Join/Request/Result messages,
+ * the server's scheduler) is unchanged by this library.
+ *
+ * Conventions
+ *   - Every function returns an int status: BM_OK (0) or a negative BM_E*
+ *     code; bm_strerror() names it.  Nothing aborts.  On failure the output
+ *     arguments are left untouched.
+ *   - msg is a raw byte string (Go's "%s" of a string: no escaping, may hold
+ *     any byte).  The library copies what it needs before returning and keeps
+ *     no caller pointer.
+ *   - Ranges are INCLUSIVE [lower, upper] (project2/README.md:329,
+ *     "0 <= n <= N").  upper = 2^64-1 is legal.  lower > upper is an empty
+ *     range and yields {2^64-1, 2^64-1}, which is what miner.go:45-46 returns
+ *     when its loop runs zero times.  (miner.go:59 itself loops i < Upper; a
+ *     caller that wants that literal behaviour passes upper-1.)
+ *   - Results are bit-exact with the reference scan: the minimum hash, and on
+ *     ties the smallest nonce (strict '<' over ascending nonces, miner.go:61).
+ *   - A context is not re-entrant: use one per OS thread or serialise calls.
+ *     Calls are synchronous.  The caller's current HIP device is restored
+ *     before each call returns.
+ *   - The compute path is the gfx950 HIP kernels only.  There is no CPU
+ *     fallback: without a usable GPU, bm_ctx_create() fails with BM_ENODEV.
+ */
+#ifndef BTCMINER_H
+#define BTCMINER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BM_ABI_VERSION 1
+
+/* status codes */
+#define BM_OK 0
+#define BM_EINVAL (-1)   /* bad argument (NULL pointer, msg too long, ...) */
+#define BM_ENODEV (-2)   /* no usable gfx950 device / device id out of range */
+#define BM_EHIP (-3)     /* a HIP runtime call failed */
+#define BM_ERCCL (-4)    /* an RCCL call failed (multi-GPU contexts) */
+#define BM_ENOMEM (-5)   /* host or device allocation failed */
+#define BM_EINTERNAL (-6)/* planner invariant violated (a bug) */
+
+#define BM_MAX_MSG_LEN (1u << 20) /* bytes; LSP payloads are ~1 KB (README:61) */
+
+/* The 16-byte result of a search: {Hash, Nonce} of bitcoin.NewResult
+ * (bitcoin/message.go:36-42).  Ordered lexicographically (hash, nonce). */
+typedef struct bm_result {
+    uint64_t hash;
+    uint64_t nonce;
+} bm_result_t;
+
+typedef struct bm_ctx bm_ctx_t;
+
+int bm_abi_version(void);
+const char* bm_strerror(int status);
+
+/* Number of visible HIP devices (0 when there is none). */
+int bm_device_count(int* out);
+
+/* Context over devices 0..num_gpus-1 (num_gpus = 0: all visible devices).
+ * A context with several devices splits every search across them and
+ * combines the per-device 16-byte partials with one RCCL allgather. */
+int bm_ctx_create(int num_gpus, bm_ctx_t** out);
+/* Context over an explicit device list (e.g. {LOCAL_RANK} for one process
+ * per GPU). */
+int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out);
+int bm_ctx_destroy(bm_ctx_t* ctx);
+int bm_ctx_num_devices(const bm_ctx_t* ctx, int* out);
+
+/* The hot path: min over n in [lower, upper] of (Hash(msg, n), n).
+ * Replaces miner.go:58-65 (+ hash.go:11-15 per nonce). */
+int bm_search_gpu(bm_ctx_t* ctx, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper,
+                  bm_result_t* out);
+
+/* Batched bitcoin.Hash (hash.go:11-15) on the first device of ctx:
+ * out[i] = Hash(msg, nonces[i]) for i < n. */
+int bm_hash_gpu(bm_ctx_t* ctx, const uint8_t* msg, size_t len, const uint64_t* nonces, size_t n,
+                uint64_t* out);
+
+/* ---- measurement (used by bench.py; does not change results) ---------- */
+
+#define BM_MAX_LAUNCH_STATS 64
+
+typedef struct bm_launch_stat {
+    int32_t device;       /* index into the context's device list */
+    int32_t p;            /* byte position of the last digit in its SHA block */
+    int32_t nbv;          /* varying blocks per task (1 or 2) */
+    int32_t pad_block;    /* 1 when a constant padding block follows */
+    int32_t digits;       /* decimal digits of every nonce in the launch */
+    int32_t inner_digits; /* digits iterated by each thread's inner loop */
+    uint64_t nonces;      /* nonces the launch is responsible for */
+    uint32_t grid;        /* workgroups launched (256 threads each) */
+    uint32_t tasks_per_thread;
+    double ms;            /* launch duration from HIP events on its stream (0 if timing off) */
+} bm_launch_stat_t;
+
+typedef struct bm_stats {
+    uint32_t launches;     /* search-kernel launches of the last call */
+    uint32_t recorded;     /* entries filled in launch[] (<= BM_MAX_LAUNCH_STATS) */
+    double wall_ms;        /* host wall time of the last bm_search_gpu call */
+    double kernel_ms;      /* sum of launch durations (timing on) */
+    uint64_t nonces;       /* nonces in the last call */
+    bm_launch_stat_t launch[BM_MAX_LAUNCH_STATS];
+} bm_stats_t;
+
+/* Enable per-launch HIP event timing (default off). */
+int bm_ctx_set_timing(bm_ctx_t* ctx, int enable);
+int bm_ctx_last_stats(const bm_ctx_t* ctx, bm_stats_t* out);
+
+/* Occupancy override for the search kernels: workgroups of 256 threads kept
+ * resident per CU (0 = ask the runtime).  Exposed for tuning. */
+int bm_ctx_set_blocks_per_cu(bm_ctx_t* ctx, int blocks_per_cu);
+
+/* Planner knob: a digit-count segment whose high digits take more than
+ * max_windows distinct values is run as ONE launch whose tasks re-compress
+ * the block holding them (nbv = 2) instead of one launch per value
+ * (default 64; 0 forces nbv = 2 wherever the digits straddle a block).
+ * Results do not depend on it. */
+int bm_ctx_set_max_windows(bm_ctx_t* ctx, int max_windows);
+
+/* ---- host-side plan introspection (pure CPU; used by the CPU tests) ---- */
+
+/* One kernel launch of a search: every nonce n = nonce_base + v with v in
+ * [vlo, vhi] has exactly `digits` decimal digits and a message whose bytes
+ * before the varying SHA-256 block(s) are constant (folded into mid[]). */
+typedef struct bm_segment {
+    int32_t p;            /* byte index of the last digit inside the last varying block */
+    int32_t nbv;          /* varying blocks (1, or 2 when a task also re-compresses the block before) */
+    int32_t pad_block;    /* 1: a constant padding block follows the varying block */
+    int32_t digits;       /* decimal digits of every nonce */
+    int32_t nd;           /* digits of v that live in the varying block(s) */
+    int32_t max_inner;    /* max digits the inner loop may iterate (all in one word) */
+    uint64_t vlo, vhi;    /* inclusive range of v */
+    uint64_t nonce_base;  /* nonce = nonce_base + v */
+    uint32_t mid[8];      /* SHA-256 state before the varying block(s) */
+    uint32_t tmpl[32];    /* varying block words, big-endian, digit bytes = '0' */
+    uint32_t pad_w[16];   /* words of the constant padding block (pad_block) */
+} bm_segment_t;
+
+/* Fill up to cap segments for (msg, [lower, upper]); *nseg gets the count
+ * needed (call with cap = 0 to size). */
+int bm_plan_segments(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper,
+                     bm_segment_t* segs, int cap, int* nseg);
+/* Same with an explicit max_windows (see bm_ctx_set_max_windows). */
+int bm_plan_segments_ex(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, int max_windows,
+                        bm_segment_t* segs, int cap, int* nseg);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BTCMINER_H */

@@ -1,0 +1,55 @@
+"""The C ABI (include/btcminer.h) on a host without a GPU: the library
+loads, exports every declared function, and fails loudly (BM_ENODEV) rather
+than falling back to a CPU path."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+from distributed_bitcoin_minter_amd import _lib
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "btcminer.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(bm_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_api():
+    names = declared_functions()
+    for required in ["bm_search_gpu", "bm_hash_gpu", "bm_ctx_create", "bm_ctx_destroy", "bm_strerror",
+                     "bm_plan_segments"]:
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_abi_version_and_errors():
+    lib = _lib.load()
+    assert lib.bm_abi_version() == 1
+    for code in range(0, -7, -1):
+        assert lib.bm_strerror(code).decode() != "unknown status"
+    assert lib.bm_strerror(-99).decode() == "unknown status"
+
+
+def test_invalid_arguments_rejected():
+    lib = _lib.load()
+    r = _lib.Result()
+    assert lib.bm_search_gpu(None, b"x", 1, 0, 1, ctypes.byref(r)) == _lib.BM_EINVAL
+    assert lib.bm_ctx_create(-1, ctypes.byref(ctypes.c_void_p())) == _lib.BM_EINVAL
+    assert lib.bm_ctx_destroy(None) == _lib.BM_EINVAL
+    n = ctypes.c_int()
+    assert lib.bm_plan_segments(b"x", 1, 0, 1, None, 1, ctypes.byref(n)) == _lib.BM_EINVAL
+
+
+@pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")
+def test_no_gpu_fails_loudly():
+    with pytest.raises(_lib.BtcMinerError) as ei:
+        _lib.Context(num_gpus=1)
+    assert ei.value.status == _lib.BM_ENODEV

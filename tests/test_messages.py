@@ -1,0 +1,42 @@
+"""The bitcoin message API mirror (bitcoin/message.go) and the Go JSON
+wire form it travels in (LSP payloads)."""
+import json
+
+import pytest
+
+from distributed_bitcoin_minter_amd.bitcoin import (Message, MsgType, NewJoin, NewRequest, NewResult, U64_MAX,
+                                                    go_json_string)
+
+
+def test_constructors_and_string():
+    # message.go:25-60
+    assert NewRequest("msg", 0, 2).String() == "[Request msg 0 2]"
+    assert NewResult(4754799531757243342, 1).String() == "[Result 4754799531757243342 1]"
+    assert NewJoin().String() == "[Join]"
+    assert (MsgType.Join, MsgType.Request, MsgType.Result) == (0, 1, 2)
+
+
+def test_marshal_matches_go_struct_layout():
+    raw = NewRequest("bradfitz", 0, 9999).marshal()
+    assert raw == b'{"Type":1,"Data":"bradfitz","Lower":0,"Upper":9999,"Hash":0,"Nonce":0}'
+    assert json.loads(raw)["Upper"] == 9999
+    big = NewResult(U64_MAX, U64_MAX).marshal()
+    assert b"18446744073709551615" in big
+
+
+def test_roundtrip_and_zero_defaults():
+    m = NewRequest("a <b> & \"c\"\n", 7, U64_MAX)
+    assert Message.unmarshal(m.marshal()) == m
+    # fields absent from the JSON keep Go's zero values
+    assert Message.unmarshal(b'{"Type":2,"Hash":5}') == NewResult(5, 0)
+
+
+def test_go_html_escaping():
+    assert go_json_string("<&>") == '"\\u003c\\u0026\\u003e"'
+    assert go_json_string(" ") == '"\\u2028"'
+    assert go_json_string("é") == '"é"'
+
+
+def test_rejects_out_of_range():
+    with pytest.raises(ValueError):
+        Message.unmarshal(b'{"Type":1,"Lower":18446744073709551616}')

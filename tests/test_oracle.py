@@ -1,0 +1,61 @@
+"""The CPU oracle (oracle/bm_oracle.c) against the golden fixtures.
+
+Pins the oracle before it is trusted as the checker: README:331-335 known
+answers, 1,000 hashlib Hash vectors, hashlib min-scan vectors at block and
+digit-count edges, and the whole-range answers of C1/C2/C3.
+"""
+import os
+
+import pytest
+
+from conftest import U64, load_golden
+
+
+def test_readme_known_answers(oracle):
+    ka = load_golden("known_answers.json")
+    for e in ka["hash"]:
+        assert oracle.hash(e["msg"].encode(), e["nonce"]) == e["hash"]
+    for e in ka["search"]:
+        assert oracle.search(e["msg"].encode(), e["lower"], e["upper"]) == (e["hash"], e["nonce"])
+
+
+def test_hash_vectors(oracle):
+    for v in load_golden("hash_vectors.json")["vectors"]:
+        assert oracle.hash(bytes.fromhex(v["msg_hex"]), v["nonce"]) == v["hash"], v
+
+
+def test_search_vectors(oracle):
+    for c in load_golden("search_vectors.json")["cases"]:
+        msg = bytes.fromhex(c["msg_hex"])
+        assert oracle.search(msg, c["lower"], c["upper"]) == (c["hash"], c["nonce"]), c
+        if c["upper"] - c["lower"] < 3000 and c["lower"] <= c["upper"]:
+            assert oracle.search(msg, c["lower"], c["upper"], threads=3) == (c["hash"], c["nonce"])
+
+
+def test_exclusive_upper_matches_miner_go_loop(oracle):
+    # miner.go:59 `for i := Lower; i < Upper; i++`
+    msg = b"bradfitz"
+    assert oracle.search_excl(msg, 0, 10000) == oracle.search(msg, 0, 9999)
+    assert oracle.search_excl(msg, 5, 5) == (U64, U64)
+
+
+def test_full_range_goldens(oracle):
+    """C1 recomputed; C2/C3 answers re-hashed and their neighbourhood
+    re-scanned (the whole 2^32 scans take ~1 min each on 8 cores: set
+    BM_FULL_ORACLE=1 to recompute them)."""
+    full = os.environ.get("BM_FULL_ORACLE") == "1"
+    for c in load_golden("full_range.json")["cases"]:
+        msg = bytes.fromhex(c["msg_hex"])
+        lo, hi, h, n = c["lower"], c["upper"], c["hash"], c["nonce"]
+        assert oracle.hash(msg, n) == h
+        if c["config"] == "C1" or full:
+            assert oracle.search(msg, lo, hi, threads=8, openssl=True) == (h, n)
+        else:
+            a, b = max(lo, n - 50000), min(hi, n + 50000)
+            assert oracle.search(msg, a, b, threads=8) == (h, n)
+
+
+def test_openssl_and_scalar_agree(oracle):
+    msg = b"The quick brown fox"
+    for lo, hi in [(0, 5000), (U64 - 5000, U64), (999_999_000, 1_000_001_000)]:
+        assert oracle.search(msg, lo, hi, threads=4, openssl=True) == oracle.search(msg, lo, hi)

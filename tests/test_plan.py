@@ -1,0 +1,134 @@
+"""CPU tests of the host-side launch planner (bm_plan_segments).
+
+The GPU kernel consumes each segment as: template words + the digits of v
+added at byte 64*(nbv-1) + p - i, compressed from the segment's midstate
+(plus the constant padding block), and assumes the words after the last
+digit word are the compile-time constants of bm_kernels.hpp:tail_word().
+These tests replay exactly that on the CPU (pure-Python SHA-256) and check
+it against hashlib's SHA-256 of "msg nonce" (hash.go:13), so a layout bug is
+caught here, without a GPU.
+"""
+import hashlib
+import random
+
+import pytest
+
+from distributed_bitcoin_minter_amd import plan_segments
+from sharef import IV, compress
+
+U64 = (1 << 64) - 1
+
+
+def ref_hash(msg, n):
+    return int.from_bytes(hashlib.sha256(msg + b" " + str(n).encode()).digest()[:8], "big")
+
+
+def kernel_replay(seg, v):
+    words = list(seg.tmpl)[: 16 * seg.nbv]
+    for i in range(seg.nd):
+        pos = 64 * (seg.nbv - 1) + seg.p - i
+        words[pos >> 2] += ((v // 10 ** i) % 10) << (8 * (3 - (pos & 3)))
+    st = list(seg.mid)
+    for b in range(seg.nbv):
+        st = compress(st, words[16 * b: 16 * b + 16])
+    if seg.pad_block:
+        st = compress(st, list(seg.pad_w))
+    return (st[0] << 32) | st[1]
+
+
+def tail_word(p, pad):
+    """Mirror of bm_kernels.hpp tail_word<P, PADB>(k): None = runtime."""
+    lw = p // 4
+
+    def f(k):
+        if k == lw + 1 and p % 4 == 3 and p != 63:
+            return 0x80000000
+        if not pad and k == 15:
+            return None
+        return 0
+    return f
+
+
+def check_plan(msg, lo, hi, rng, samples=6):
+    segs = plan_segments(msg, lo, hi)
+    # segments tile [lo, hi] in ascending order
+    cur = lo
+    for s in segs:
+        a, b = s.nonce_base + s.vlo, s.nonce_base + s.vhi
+        assert a == cur and a <= b
+        assert len(str(a)) == len(str(b)) == s.digits
+        cur = b + 1
+    assert cur - 1 == hi
+    for s in segs:
+        assert s.nbv in (1, 2) and 0 <= s.p < 64
+        assert s.pad_block == (1 if (s.nbv == 1 and s.p >= 55) else 0)
+        if s.nbv == 2:
+            assert s.p <= 18
+        assert s.vhi < 10 ** s.nd
+        # compile-time words of the kernel match the template
+        tw = tail_word(s.p, bool(s.pad_block))
+        base = 16 * (s.nbv - 1)
+        for k in range(s.p // 4 + 1, 16):
+            exp = tw(k)
+            if exp is not None:
+                assert s.tmpl[base + k] == exp, (s.p, k)
+        # the inner-loop digits all sit in the last-digit word
+        for i in range(s.max_inner):
+            assert (s.p - i) // 4 == s.p // 4
+        vs = {s.vlo, s.vhi, (s.vlo + s.vhi) // 2}
+        for _ in range(samples):
+            vs.add(rng.randint(s.vlo, s.vhi))
+        for v in vs:
+            assert kernel_replay(s, v) == ref_hash(msg, s.nonce_base + v), (len(msg), s.nonce_base + v)
+    return segs
+
+
+RANGES = [(0, 9999), (0, 2 ** 32 - 1), (9990, 10009), (U64 - 2 ** 32 + 1, U64), (10 ** 19 - 5, 10 ** 19 + 5),
+          (0, U64), (123456789, 123456789), (5, 5)]
+
+
+@pytest.mark.parametrize("L", [0, 1, 7, 8, 30, 44, 45, 46, 53, 54, 55, 56, 57, 62, 63, 64, 65, 100, 110, 118, 119,
+                               120, 121, 127, 128, 183, 600])
+def test_plan_layout_matches_sha256(L):
+    rng = random.Random(L)
+    msg = bytes(rng.choice(b"abcdefghijklmnopqrstuvwxyz ,.-") for _ in range(L))
+    for lo, hi in RANGES:
+        check_plan(msg, lo, hi, rng)
+
+
+def test_plan_every_layout_reachable():
+    """Across message lengths 0..127 the planner emits every layout the
+    kernel table instantiates (NBV=1: P 0..63; NBV=2: P 0..18)."""
+    seen = set()
+    for L in range(128):
+        msg = b"x" * L
+        for lo, hi in [(0, U64)]:
+            for s in plan_segments(msg, lo, hi):
+                seen.add((s.nbv, s.p))
+    assert {(1, p) for p in range(64)} <= seen
+    # NBV=2 shows up when the high digits straddle a block boundary over
+    # more than 64 windows; with 10^17..10^19-nonce windows that never
+    # happens, so P 17/18 (instantiated for safety) are unreachable.
+    for L in range(40, 64):
+        for s in plan_segments(b"y" * L, 0, U64):
+            seen.add((s.nbv, s.p))
+    assert {(2, p) for p in range(17)} <= seen
+    assert all(p <= 16 for nbv, p in seen if nbv == 2)
+
+
+def test_plan_empty_and_bad_args():
+    assert plan_segments(b"msg", 10, 9) == []
+    from distributed_bitcoin_minter_amd._lib import BtcMinerError
+    with pytest.raises(BtcMinerError):
+        plan_segments(b"x" * ((1 << 20) + 1), 0, 1)
+
+
+def test_plan_c3_single_window():
+    """C3 (120-B msg, 20-digit nonces near 2^64): the 7 high digits in the
+    second block are constant over the range, so one launch with them in the
+    midstate and 1 compression per nonce."""
+    msg = (b"The quick brown fox jumps over the lazy dog. " * 3)[:120]
+    segs = plan_segments(msg, U64 - (2 ** 32 - 1), U64)
+    assert len(segs) == 1
+    s = segs[0]
+    assert (s.nbv, s.p, s.pad_block, s.digits, s.nd) == (1, 12, 0, 20, 13)
