@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbtcminer.so")
+# BTCMINER_LIB overrides the library path (used to A/B kernel build variants)
+LIB_PATH = os.environ.get("BTCMINER_LIB") or os.path.join(_HERE, "libbtcminer.so")
 
 BM_OK = 0
 BM_EINVAL = -1

@@ -23,7 +23,8 @@ namespace bm {
 // search kernel table [nbv-1][P], filled by bm_inst.hip at load time
 static const void* g_search[2][64];
 
-constexpr int kTasksPerThreadTarget = 16;  // balance: tasks per thread before growing S
+constexpr int kMaxInnerDigits = 2;  // S <= 100 nonces per task: small dequeue chunks, short tail
+constexpr uint32_t kNoncesPerLaneChunk = 100;
 constexpr int kEventPairs = BM_MAX_LAUNCH_STATS;
 
 struct DeviceCtx {
@@ -32,6 +33,8 @@ struct DeviceCtx {
     hipStream_t stream = nullptr;
     Partial* d_part = nullptr;
     size_t part_cap = 0;
+    unsigned long long* d_ctr = nullptr;  // one dequeue counter per launch
+    size_t ctr_cap = 0;
     Partial* d_result = nullptr;  // 1 partial
     Partial* d_gather = nullptr;  // n_dev partials (allgather target)
     Partial* h_result = nullptr;  // pinned, n_dev partials
@@ -98,29 +101,21 @@ int blocks_per_cu(bm_ctx* ctx, DeviceCtx& d, const void* fn) {
     return nb;
 }
 
-// Size one launch: S = 10^ms nonces per task, tasks spread evenly over a
-// grid that is fully resident (grid-stride, every thread the same count
-// +-1), so the launch drains together.
+// Size one launch: S = 10^ms nonces per task (ms <= digits of word LW),
+// chunks of 64*m tasks dequeued per wave, and at most one resident grid of
+// workgroups (any surplus workgroup simply finds the counter exhausted).
 int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_off, Launch& L) {
     const void* fn = g_search[s.nbv - 1][s.p];
     if (!fn) return BM_EINTERNAL;
-    const uint64_t gmax = (uint64_t)blocks_per_cu(ctx, d, fn) * (uint64_t)d.cus * kBlock;
-    int ms = 1;
-    for (int m = s.max_inner; m >= 1; --m) {
-        const uint64_t S = kPow10[m];
-        const uint64_t T = s.vhi / S - s.vlo / S + 1;
-        if (T >= (uint64_t)kTasksPerThreadTarget * gmax) {
-            ms = m;
-            break;
-        }
-    }
+    const int ms = std::max(1, std::min(s.max_inner, kMaxInnerDigits));
     const uint64_t S = kPow10[ms];
+    const uint32_t m = (uint32_t)std::max<uint64_t>(1, kNoncesPerLaneChunk / S);
     const uint64_t t0 = s.vlo / S, t_end = s.vhi / S + 1;
     const uint64_t T = t_end - t0;
-    const uint64_t k = (T + gmax - 1) / gmax;       // tasks per thread
-    const uint64_t G = (T + k - 1) / k;             // threads needed
-    const uint64_t grid = (G + kBlock - 1) / kBlock;
-    if (grid == 0 || grid > 0x7fffffffull) return BM_EINTERNAL;
+    const uint64_t chunks = (T + 64ull * m - 1) / (64ull * m);
+    const uint64_t resident = (uint64_t)blocks_per_cu(ctx, d, fn) * (uint64_t)d.cus;
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, resident));
+    const uint64_t k = (chunks + grid * 4 - 1) / (grid * 4);  // chunks per wave (approx.)
 
     SearchArgs& A = L.args;
     std::memset(&A, 0, sizeof A);
@@ -137,7 +132,7 @@ int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_
     A.nonce_base = s.nonce_base;
     A.t0 = t0;
     A.t_end = t_end;
-    A.stride = grid * kBlock;
+    A.chunk_m = m;
     A.S = (uint32_t)S;
     A.ms = (uint32_t)ms;
     A.nd = (uint32_t)s.nd;
@@ -152,7 +147,18 @@ int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_
     L.stat.inner_digits = ms;
     L.stat.nonces = s.vhi - s.vlo + 1;
     L.stat.grid = (uint32_t)grid;
-    L.stat.tasks_per_thread = (uint32_t)k;
+    L.stat.tasks_per_thread = (uint32_t)(k * m);
+    return BM_OK;
+}
+
+int ensure_counters(DeviceCtx& d, size_t n) {
+    if (n <= d.ctr_cap) return BM_OK;
+    if (d.d_ctr) BM_HIP(hipFree(d.d_ctr));
+    d.d_ctr = nullptr;
+    d.ctr_cap = 0;
+    size_t cap = std::max<size_t>(n, 256);
+    BM_HIP(hipMalloc(&d.d_ctr, cap * sizeof(unsigned long long)));
+    d.ctr_cap = cap;
     return BM_OK;
 }
 
@@ -179,6 +185,8 @@ int init_device(DeviceCtx& d, int id, int ndev) {
     BM_HIP(hipMalloc(&d.d_gather, sizeof(Partial) * (size_t)ndev));
     BM_HIP(hipHostMalloc(&d.h_result, sizeof(Partial) * (size_t)ndev, hipHostMallocDefault));
     for (auto& e : d.ev) BM_HIP(hipEventCreate(&e));
+    int rc = ensure_counters(d, 256);
+    if (rc != BM_OK) return rc;
     return ensure_partials(d, 4096);
 }
 
@@ -190,6 +198,7 @@ void destroy_device(DeviceCtx& d) {
     for (auto& e : d.ev)
         if (e) (void)hipEventDestroy(e);
     if (d.d_part) (void)hipFree(d.d_part);
+    if (d.d_ctr) (void)hipFree(d.d_ctr);
     if (d.d_result) (void)hipFree(d.d_result);
     if (d.d_gather) (void)hipFree(d.d_gather);
     if (d.d_hash_io) (void)hipFree(d.d_hash_io);
@@ -241,6 +250,8 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         BM_HIP(hipSetDevice(ctx->devs[di].id));
         rc = ensure_partials(ctx->devs[di], off);
         if (rc != BM_OK) return rc;
+        rc = ensure_counters(ctx->devs[di], launches[di].size());
+        if (rc != BM_OK) return rc;
     }
 
     // 2. enqueue: search launches, then the second-pass reduction
@@ -248,10 +259,13 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         DeviceCtx& d = ctx->devs[di];
         BM_HIP(hipSetDevice(d.id));
         uint32_t nparts = 0, li = 0;
+        if (!launches[di].empty())
+            BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches[di].size() * sizeof(unsigned long long), d.stream));
         for (Launch& L : launches[di]) {
             const bool timed = ctx->timing && li < (uint32_t)kEventPairs;
             if (timed) BM_HIP(hipEventRecord(d.ev[2 * li], d.stream));
-            void* kargs[] = {&L.args, &d.d_part};
+            unsigned long long* ctr = d.d_ctr + li;
+            void* kargs[] = {&L.args, &d.d_part, &ctr};
             BM_HIP(hipLaunchKernel(L.fn, dim3(L.grid), dim3(kBlock), kargs, 0, d.stream));
             if (timed) BM_HIP(hipEventRecord(d.ev[2 * li + 1], d.stream));
             nparts += L.grid;

@@ -20,11 +20,12 @@ struct SearchArgs {
     uint64_t vlo, vhi;   // inclusive range of v; nonce = nonce_base + v
     uint64_t nonce_base;
     uint64_t t0, t_end;  // task range [t0, t_end); task t covers v in [t*S, t*S + S)
-    uint64_t stride;     // total threads of the grid (grid-stride over tasks)
+    uint32_t chunk_m;    // tasks per lane per dequeued chunk (a chunk = 64*chunk_m tasks)
     uint32_t S;          // nonces per task = 10^ms
     uint32_t ms;         // digits iterated by the inner loop (all in one word)
     uint32_t nd;         // digits of v placed in the varying block(s)
     uint32_t part_off;   // first partial slot written by this launch
+    uint32_t pad_;
 };
 
 struct HashArgs {

@@ -216,11 +216,29 @@ BM_DEV bool block_min(uint64_t& h, uint64_t& n) {
     return false;
 }
 
+BM_DEV uint64_t readfirstlane_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // The search kernel for one layout.  P = byte index (0..63) of the last
 // digit inside the last varying block; NBV = 2 when each task also
 // re-compresses the block before it (high digits there).
+//
+// Work distribution: each wave dequeues chunks of 64*m consecutive tasks
+// from a per-launch counter (one returning atomic per chunk, lane 0), lane l
+// taking tasks base + l, base + 64 + l, ...  Chunks come out of the counter in
+// increasing order, so every lane still visits its nonces in ascending order
+// (required for the strict-'<' tie rule), and the launch drains within one
+// chunk whatever the residency or clock of each CU.
+#ifndef BM_KATTR  // occupancy request of the search kernels (a build knob; see Makefile)
+#define BM_KATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#endif
+
 template <int P, int NBV>
-__global__ __launch_bounds__(kBlock) void search_kernel(const SearchArgs A, Partial* __restrict__ part) {
+__global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
+    const SearchArgs A, Partial* __restrict__ part, unsigned long long* __restrict__ counter) {
     static_assert(P >= 0 && P < 64 && (NBV == 1 || (NBV == 2 && P <= 18)), "layout");
     constexpr int LW = P / 4;                      // last-block word holding the last digit
     constexpr int BOFF = 16 * (NBV - 1);           // word offset of the last block
@@ -237,94 +255,108 @@ __global__ __launch_bounds__(kBlock) void search_kernel(const SearchArgs A, Part
     uint32_t bh = 0xFFFFFFFFu;  // high word of best_h
 
     const uint32_t S = A.S;
-    for (uint64_t t = A.t0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < A.t_end; t += A.stride) {
-        // ---- per task: words, block before (NBV=2), rounds 0..LW-1 ----
-        uint32_t W[16 * NBV];
-        static_for<0, 16 * NBV>([&](auto K) { W[decltype(K)::value] = A.tmpl[decltype(K)::value]; });
-        add_task_digits<P, NBV>(W, t, A.ms, A.nd);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t ntask = A.t_end - A.t0;
+    const uint64_t chunk = 64ull * A.chunk_m;
 
-        uint32_t st[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) st[i] = A.mid[i];
-        if constexpr (NBV == 2) {
-            uint32_t wa[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) wa[k] = W[k];
-            sha_compress(st, wa);
-        }
+    for (;;) {
+        uint64_t base = 0;
+        if (lane == 0) base = atomicAdd(counter, (unsigned long long)chunk);
+        base = readfirstlane_u64(base);
+        if (base >= ntask) break;
+        for (uint32_t i = 0; i < A.chunk_m; ++i) {
+            const uint64_t tt = base + 64ull * i + lane;
+            if (tt >= ntask) break;
+            const uint64_t t = A.t0 + tt;
 
-        uint32_t wb[16];
-        static_for<0, 16>([&](auto K) {
-            constexpr int k = decltype(K)::value;
-            if constexpr (k <= LW) {
-                wb[k] = W[BOFF + k];
-            } else {
-                constexpr int64_t c = tail_word<P, PADB>(k);
-                if constexpr (c < 0)
-                    wb[k] = A.tmpl[BOFF + k];
-                else
-                    wb[k] = (uint32_t)c;
-            }
-        });
-        uint32_t s0[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s0[i] = st[i];
-        sha_rounds<0, LW>(s0, wb);
-        const uint32_t wl = wb[LW];
+            // ---- per task: words, block before (NBV=2), rounds 0..LW-1 ----
+            uint32_t W[16 * NBV];
+            static_for<0, 16 * NBV>([&](auto K) { W[decltype(K)::value] = A.tmpl[decltype(K)::value]; });
+            add_task_digits<P, NBV>(W, t, A.ms, A.nd);
 
-        // ---- inner loop over the ms uniform low digits ----
-        const uint64_t vbase = t * (uint64_t)S;
-        uint32_t J = 0, c0 = 0, c1 = 0, c2 = 0;
-        for (uint32_t j = 0; j < S; ++j) {
-            uint32_t w[16];
+            uint32_t st[8];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) w[k] = wb[k];
-            w[LW] = wl + J;
-            uint32_t x[8];
+            for (int q = 0; q < 8; ++q) st[q] = A.mid[q];
+            if constexpr (NBV == 2) {
+                uint32_t wa[16];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = s0[i];
-            sha_rounds<LW, 64>(x, w);
-
-            uint32_t h0, h1;
-            if constexpr (PADB) {
-                uint32_t y[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) y[i] = st[i] + x[i];
-                uint32_t z[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) z[i] = y[i];
-                static_for<0, 64>([&](auto I) {
-                    constexpr int tt = decltype(I)::value;
-                    sha_round_kw<tt>(z, A.padkw[tt]);
-                });
-                h0 = y[0] + z[0];
-                h1 = y[1] + z[1];
-            } else {
-                h0 = st[0] + x[0];
-                h1 = st[1] + x[1];
+                for (int k = 0; k < 16; ++k) wa[k] = W[k];
+                sha_compress(st, wa);
             }
 
-            if (__builtin_expect(h0 <= bh, 0)) {
-                const uint64_t h = ((uint64_t)h0 << 32) | h1;
-                const uint64_t v = vbase + j;
-                if (h < best_h && v >= A.vlo && v <= A.vhi) {
-                    best_h = h;
-                    best_n = A.nonce_base + v;
-                    bh = h0;
+            uint32_t wb[16];
+            static_for<0, 16>([&](auto K) {
+                constexpr int k = decltype(K)::value;
+                if constexpr (k <= LW) {
+                    wb[k] = W[BOFF + k];
+                } else {
+                    constexpr int64_t c = tail_word<P, PADB>(k);
+                    if constexpr (c < 0)
+                        wb[k] = A.tmpl[BOFF + k];
+                    else
+                        wb[k] = (uint32_t)c;
                 }
-            }
+            });
+            uint32_t s0[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s0[q] = st[q];
+            sha_rounds<0, LW>(s0, wb);
+            const uint32_t wl = wb[LW];
 
-            // step the uniform decimal counter held in word LW
-            J += inc0;
-            if (++c0 == 10u) {
-                c0 = 0;
-                J += inc1 - 10u * inc0;
-                if (++c1 == 10u) {
-                    c1 = 0;
-                    J += inc2 - 10u * inc1;
-                    if (++c2 == 10u) {
-                        c2 = 0;
-                        J += inc3 - 10u * inc2;
+            // ---- inner loop over the ms uniform low digits ----
+            const uint64_t vbase = t * (uint64_t)S;
+            uint32_t J = 0, c0 = 0, c1 = 0, c2 = 0;
+            for (uint32_t j = 0; j < S; ++j) {
+                uint32_t w[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) w[k] = wb[k];
+                w[LW] = wl + J;
+                uint32_t x[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) x[q] = s0[q];
+                sha_rounds<LW, 64>(x, w);
+
+                uint32_t h0, h1;
+                if constexpr (PADB) {
+                    uint32_t y[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) y[q] = st[q] + x[q];
+                    uint32_t z[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) z[q] = y[q];
+                    static_for<0, 64>([&](auto I) {
+                        constexpr int tt2 = decltype(I)::value;
+                        sha_round_kw<tt2>(z, A.padkw[tt2]);
+                    });
+                    h0 = y[0] + z[0];
+                    h1 = y[1] + z[1];
+                } else {
+                    h0 = st[0] + x[0];
+                    h1 = st[1] + x[1];
+                }
+
+                if (__builtin_expect(h0 <= bh, 0)) {
+                    const uint64_t h = ((uint64_t)h0 << 32) | h1;
+                    const uint64_t v = vbase + j;
+                    if (h < best_h && v >= A.vlo && v <= A.vhi) {
+                        best_h = h;
+                        best_n = A.nonce_base + v;
+                        bh = h0;
+                    }
+                }
+
+                // step the uniform decimal counter held in word LW
+                J += inc0;
+                if (++c0 == 10u) {
+                    c0 = 0;
+                    J += inc1 - 10u * inc0;
+                    if (++c1 == 10u) {
+                        c1 = 0;
+                        J += inc2 - 10u * inc1;
+                        if (++c2 == 10u) {
+                            c2 = 0;
+                            J += inc3 - 10u * inc2;
+                        }
                     }
                 }
             }

@@ -101,7 +101,7 @@ typedef struct bm_launch_stat {
     int32_t inner_digits; /* digits iterated by each thread's inner loop */
     uint64_t nonces;      /* nonces the launch is responsible for */
     uint32_t grid;        /* workgroups launched (256 threads each) */
-    uint32_t tasks_per_thread;
+    uint32_t tasks_per_thread; /* approx. tasks per lane (dynamic dequeue) */
     double ms;            /* launch duration from HIP events on its stream (0 if timing off) */
 } bm_launch_stat_t;
 
