@@ -52,6 +52,22 @@ def compressions_per_nonce(msg_len, digits):
     return -(-(msg_len + digits + 10) // 64) - (msg_len + 1) // 64
 
 
+def instruction_mix_ceiling(p, nbv=1, clock_ghz=2.37):
+    """gfx950 issue-cost ceiling of the kernel's inner loop:
+    slow VALU (v_alignbit, v_add3, SGPR operands, ...) 4 SIMD-cycles, fast
+    2.24, from tools/isa_mix.py's static count of the compiled loop and the
+    clock measured under this kernel (GRBM_GUI_ACTIVE, profiles/r01)."""
+    path = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc", "isa_mix.json")
+    try:
+        lay = json.load(open(path))["layouts"][f"{p}:{nbv}"]
+    except (OSError, KeyError, ValueError):
+        return None
+    cyc = lay["simd_cycles_per_64_nonces"]
+    ghs = 256 * 4 * clock_ghz * 1e9 * 64 / cyc / 1e9
+    return {"valu_per_nonce": lay["valu"], "slow": lay["valu_slow"], "fast": lay["valu_fast"],
+            "clock_ghz": clock_ghz, "GHs_per_gpu": round(ghs, 2)}
+
+
 def cpu_baseline(target_s=10.0):
     """Time the oracle loop (test infrastructure: the CPU 'port' of
     hash.go + miner.go) on this host over a bounded sample of C2."""
@@ -139,6 +155,7 @@ def main():
     dom_ms = sum(d[1] for d in doms) / len(doms)
     C = compressions_per_nonce(len(MSG), dom_digits)
     achieved = dom_nonces * C * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
+    mix = instruction_mix_ceiling(dom_p)
     check = None
     if world == 1:
         check = list(res)  # C2 golden: (5256245051, 1626825724)
@@ -165,7 +182,9 @@ def main():
                      "kernel": f"search_kernel<P={dom_p},NBV=1> ({dom_digits}-digit nonces)",
                      "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom_nonces,
                      "ops_per_nonce": C * OPS_PER_COMPRESSION, "grid": dom_grid,
-                     "tasks_per_thread": dom_tpt, "inner_digits": dom_inner},
+                     "tasks_per_thread": dom_tpt, "inner_digits": dom_inner,
+                     "mix_ceiling": mix and dict(mix, frac=round(dom_nonces / (dom_ms * 1e-3) / 1e9
+                                                                  / mix["GHs_per_gpu"], 4))},
         "result": check,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

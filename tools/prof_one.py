@@ -1,0 +1,14 @@
+#!/usr/bin/env python3
+"""Run ONE C2 search (and optionally C3) for profiling: python tools/prof_one.py [C2|C3] [reps]"""
+import json, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from distributed_bitcoin_minter_amd import Context
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+c = {c["config"]: c for c in json.load(open(os.path.join(ROOT, "tests/golden/full_range.json")))["cases"]}[cfg]
+with Context(devices=[0]) as ctx:
+    for _ in range(reps):
+        r = ctx.search(bytes.fromhex(c["msg_hex"]), c["lower"], c["upper"])
+        assert r == (c["hash"], c["nonce"]), r
+print("ok", cfg, r)
