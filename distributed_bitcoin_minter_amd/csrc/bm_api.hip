@@ -107,7 +107,10 @@ int blocks_per_cu(bm_ctx* ctx, DeviceCtx& d, const void* fn) {
 int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_off, Launch& L) {
     const void* fn = g_search[s.nbv - 1][s.p];
     if (!fn) return BM_EINTERNAL;
-    const int ms = std::max(1, std::min(s.max_inner, kMaxInnerDigits));
+    int ms = std::max(1, std::min(s.max_inner, kMaxInnerDigits));
+    // word LW holds one digit: the kernel steps the next one in word LW-1
+    // (bm_kernels.hpp TWOW), so a task can still be 100 nonces
+    if (s.p % 4 == 0 && s.p / 4 >= 1 && s.nd >= 2) ms = 2;
     const uint64_t S = kPow10[ms];
     const uint32_t m = (uint32_t)std::max<uint64_t>(1, kNoncesPerLaneChunk / S);
     const uint64_t t0 = s.vlo / S, t_end = s.vhi / S + 1;

@@ -232,8 +232,21 @@ BM_DEV uint64_t readfirstlane_u64(uint64_t v) {
 // increasing order, so every lane still visits its nonces in ascending order
 // (required for the strict-'<' tie rule), and the launch drains within one
 // chunk whatever the residency or clock of each CU.
+// Occupancy request per layout: 8 waves/SIMD (64 VGPR, <= 80 SGPR) keeps
+// every 1-block inner loop spill-free; the layouts that carry a second
+// compression or a per-task block re-compression in registers get a larger
+// register budget (tools/check_inner.py verifies no spill lands in a loop).
+#ifndef BM_WAVES_PAD
+#define BM_WAVES_PAD 5
+#endif
+#ifndef BM_WAVES_NBV2
+#define BM_WAVES_NBV2 6
+#endif
+constexpr int search_waves(int P, int NBV) {
+    return (NBV == 1 && P >= 55) ? BM_WAVES_PAD : (NBV == 2 ? BM_WAVES_NBV2 : 8);
+}
 #ifndef BM_KATTR  // occupancy request of the search kernels (a build knob; see Makefile)
-#define BM_KATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#define BM_KATTR __attribute__((amdgpu_waves_per_eu(search_waves(P, NBV), 8)))
 #endif
 
 template <int P, int NBV>
@@ -243,6 +256,10 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
     constexpr int LW = P / 4;                      // last-block word holding the last digit
     constexpr int BOFF = 16 * (NBV - 1);           // word offset of the last block
     constexpr bool PADB = (NBV == 1) && (P >= 55); // a constant padding block follows
+    // Word LW holds only the last digit (P%4 == 0): a task's second digit is
+    // stepped by an outer loop in word LW-1 (round LW-1 redone per step), so
+    // tasks stay 100 nonces long instead of 10.
+    constexpr bool TWOW = (P % 4 == 0) && (LW >= 1);
 
     // Inner-loop digit steps: digit i (< ms) of the inner counter sits at
     // bit 8*(3 - P%4 + i) of word LW.
@@ -255,6 +272,9 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
     uint32_t bh = 0xFFFFFFFFu;  // high word of best_h
 
     const uint32_t S = A.S;
+    // TWOW: S in {10, 100} = n_out x 10; otherwise one pass of S inner steps
+    const uint32_t n_in = TWOW ? 10u : S;
+    const uint32_t n_out = TWOW ? S / 10u : 1u;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t ntask = A.t_end - A.t0;
     const uint64_t chunk = 64ull * A.chunk_m;
@@ -297,65 +317,81 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
                         wb[k] = (uint32_t)c;
                 }
             });
-            uint32_t s0[8];
+            // rounds before the varying word(s): once per task
+            constexpr int R0 = TWOW ? LW - 1 : LW;
+            uint32_t s00[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) s0[q] = st[q];
-            sha_rounds<0, LW>(s0, wb);
-            const uint32_t wl = wb[LW];
+            for (int q = 0; q < 8; ++q) s00[q] = st[q];
+            sha_rounds<0, R0>(s00, wb);
 
-            // ---- inner loop over the ms uniform low digits ----
             const uint64_t vbase = t * (uint64_t)S;
-            uint32_t J = 0, c0 = 0, c1 = 0, c2 = 0;
-            for (uint32_t j = 0; j < S; ++j) {
-                uint32_t w[16];
+            for (uint32_t jo = 0; jo < n_out; ++jo) {
+                // ---- outer step (TWOW only): digit 1 = lowest byte of word LW-1 ----
+                uint32_t wo[16];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) w[k] = wb[k];
-                w[LW] = wl + J;
-                uint32_t x[8];
+                for (int k = 0; k < 16; ++k) wo[k] = wb[k];
+                uint32_t s0[8];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) x[q] = s0[q];
-                sha_rounds<LW, 64>(x, w);
-
-                uint32_t h0, h1;
-                if constexpr (PADB) {
-                    uint32_t y[8];
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) y[q] = st[q] + x[q];
-                    uint32_t z[8];
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) z[q] = y[q];
-                    static_for<0, 64>([&](auto I) {
-                        constexpr int tt2 = decltype(I)::value;
-                        sha_round_kw<tt2>(z, A.padkw[tt2]);
-                    });
-                    h0 = y[0] + z[0];
-                    h1 = y[1] + z[1];
-                } else {
-                    h0 = st[0] + x[0];
-                    h1 = st[1] + x[1];
+                for (int q = 0; q < 8; ++q) s0[q] = s00[q];
+                if constexpr (TWOW) {
+                    wo[LW - 1] = wb[LW - 1] + jo;
+                    sha_rounds<LW - 1, LW>(s0, wo);
                 }
+                const uint32_t wl = wo[LW];
 
-                if (__builtin_expect(h0 <= bh, 0)) {
-                    const uint64_t h = ((uint64_t)h0 << 32) | h1;
-                    const uint64_t v = vbase + j;
-                    if (h < best_h && v >= A.vlo && v <= A.vhi) {
-                        best_h = h;
-                        best_n = A.nonce_base + v;
-                        bh = h0;
+                // ---- inner loop over the uniform low digit(s) of word LW ----
+                uint32_t J = 0, c0 = 0, c1 = 0, c2 = 0;
+                for (uint32_t j = 0; j < n_in; ++j) {
+                    uint32_t w[16];
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) w[k] = wo[k];
+                    w[LW] = wl + J;
+                    uint32_t x[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) x[q] = s0[q];
+                    sha_rounds<LW, 64>(x, w);
+
+                    uint32_t h0, h1;
+                    if constexpr (PADB) {
+                        uint32_t y[8];
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) y[q] = st[q] + x[q];
+                        uint32_t z[8];
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) z[q] = y[q];
+                        static_for<0, 64>([&](auto I) {
+                            constexpr int tt2 = decltype(I)::value;
+                            sha_round_kw<tt2>(z, A.padkw[tt2]);
+                        });
+                        h0 = y[0] + z[0];
+                        h1 = y[1] + z[1];
+                    } else {
+                        h0 = st[0] + x[0];
+                        h1 = st[1] + x[1];
                     }
-                }
 
-                // step the uniform decimal counter held in word LW
-                J += inc0;
-                if (++c0 == 10u) {
-                    c0 = 0;
-                    J += inc1 - 10u * inc0;
-                    if (++c1 == 10u) {
-                        c1 = 0;
-                        J += inc2 - 10u * inc1;
-                        if (++c2 == 10u) {
-                            c2 = 0;
-                            J += inc3 - 10u * inc2;
+                    if (__builtin_expect(h0 <= bh, 0)) {
+                        const uint64_t h = ((uint64_t)h0 << 32) | h1;
+                        const uint64_t v = vbase + (uint64_t)jo * n_in + j;
+                        if (h < best_h && v >= A.vlo && v <= A.vhi) {
+                            best_h = h;
+                            best_n = A.nonce_base + v;
+                            bh = h0;
+                        }
+                    }
+
+                    // step the uniform decimal counter held in word LW
+                    J += inc0;
+                    if (++c0 == 10u) {
+                        c0 = 0;
+                        J += inc1 - 10u * inc0;
+                        if (++c1 == 10u) {
+                            c1 = 0;
+                            J += inc2 - 10u * inc1;
+                            if (++c2 == 10u) {
+                                c2 = 0;
+                                J += inc3 - 10u * inc2;
+                            }
                         }
                     }
                 }
