@@ -19,6 +19,7 @@ BM_ERCCL = -4
 BM_ENOMEM = -5
 BM_EINTERNAL = -6
 BM_MAX_LAUNCH_STATS = 64
+BM_COMBINE_AUTO, BM_COMBINE_RCCL, BM_COMBINE_HOST = 0, 1, 2
 U64_MAX = (1 << 64) - 1
 
 c_u64 = ctypes.c_uint64
@@ -83,6 +84,7 @@ def load():
         "bm_ctx_last_stats": ([vp, P(Stats)], ctypes.c_int),
         "bm_ctx_set_blocks_per_cu": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_ctx_set_max_windows": ([vp, ctypes.c_int], ctypes.c_int),
+        "bm_ctx_set_combine": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_plan_segments": ([ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, P(Segment), ctypes.c_int,
                               P(ctypes.c_int)], ctypes.c_int),
         "bm_plan_segments_ex": ([ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, ctypes.c_int, P(Segment),
@@ -185,6 +187,9 @@ class Context:
 
     def set_timing(self, on: bool):
         check(self._lib.bm_ctx_set_timing(self.handle, 1 if on else 0), "bm_ctx_set_timing")
+
+    def set_combine(self, mode: int):
+        check(self._lib.bm_ctx_set_combine(self.handle, mode), "bm_ctx_set_combine")
 
     def set_max_windows(self, n: int):
         check(self._lib.bm_ctx_set_max_windows(self.handle, n), "bm_ctx_set_max_windows")

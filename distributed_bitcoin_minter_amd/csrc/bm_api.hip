@@ -80,6 +80,7 @@ struct bm_ctx {
     bool timing = false;
     int blocks_per_cu = 0;
     int max_windows = bm::kDefaultMaxWindows;
+    int combine = BM_COMBINE_AUTO;
     bool nccl_ready = false;
     bm_stats_t stats;
 };
@@ -210,7 +211,7 @@ void destroy_device(DeviceCtx& d) {
 }
 
 int ensure_nccl(bm_ctx* ctx) {
-    if (ctx->nccl_ready || ctx->devs.size() < 2) return BM_OK;
+    if (ctx->nccl_ready) return BM_OK;
     const int n = (int)ctx->devs.size();
     std::vector<ncclComm_t> comms(n);
     std::vector<int> ids(n);
@@ -278,8 +279,9 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         BM_HIP(hipGetLastError());
     }
 
-    // 3. combine: one RCCL allgather of the 16-byte partials, or a plain copy
-    if (ndev > 1) {
+    // 3. combine: one RCCL allgather of the 16-byte partials, or plain copies
+    const bool use_rccl = ctx->combine == BM_COMBINE_RCCL || (ctx->combine == BM_COMBINE_AUTO && ndev > 1);
+    if (use_rccl) {
         int rc = ensure_nccl(ctx);
         if (rc != BM_OK) return rc;
         if (ncclGroupStart() != ncclSuccess) return BM_ERCCL;
@@ -295,8 +297,12 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         BM_HIP(hipSetDevice(d0.id));
         BM_HIP(hipMemcpyAsync(d0.h_result, d0.d_gather, sizeof(Partial) * ndev, hipMemcpyDeviceToHost, d0.stream));
     } else {
-        DeviceCtx& d0 = ctx->devs[0];
-        BM_HIP(hipMemcpyAsync(d0.h_result, d0.d_result, sizeof(Partial), hipMemcpyDeviceToHost, d0.stream));
+        for (int di = 0; di < ndev; ++di) {
+            DeviceCtx& d = ctx->devs[di];
+            BM_HIP(hipSetDevice(d.id));
+            BM_HIP(hipMemcpyAsync(ctx->devs[0].h_result + di, d.d_result, sizeof(Partial), hipMemcpyDeviceToHost,
+                                  d.stream));
+        }
     }
     for (int di = 0; di < ndev; ++di) {
         BM_HIP(hipSetDevice(ctx->devs[di].id));
@@ -482,6 +488,12 @@ int bm_ctx_last_stats(const bm_ctx_t* ctx, bm_stats_t* out) {
 int bm_ctx_set_blocks_per_cu(bm_ctx_t* ctx, int blocks_per_cu) {
     if (!ctx || blocks_per_cu < 0 || blocks_per_cu > 32) return BM_EINVAL;
     ctx->blocks_per_cu = blocks_per_cu;
+    return BM_OK;
+}
+
+int bm_ctx_set_combine(bm_ctx_t* ctx, int mode) {
+    if (!ctx || mode < BM_COMBINE_AUTO || mode > BM_COMBINE_HOST) return BM_EINVAL;
+    ctx->combine = mode;
     return BM_OK;
 }
 

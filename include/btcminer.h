@@ -129,6 +129,16 @@ int bm_ctx_set_blocks_per_cu(bm_ctx_t* ctx, int blocks_per_cu);
  * Results do not depend on it. */
 int bm_ctx_set_max_windows(bm_ctx_t* ctx, int max_windows);
 
+/* How a context combines its per-device 16-byte partials:
+ * BM_COMBINE_AUTO (default): RCCL allgather when the context has > 1 device,
+ * a plain device-to-host copy otherwise; BM_COMBINE_RCCL: always RCCL (also
+ * for one device: exercises the collective path on a single GPU);
+ * BM_COMBINE_HOST: device-to-host copies of every partial, no RCCL. */
+#define BM_COMBINE_AUTO 0
+#define BM_COMBINE_RCCL 1
+#define BM_COMBINE_HOST 2
+int bm_ctx_set_combine(bm_ctx_t* ctx, int mode);
+
 /* ---- host-side plan introspection (pure CPU; used by the CPU tests) ---- */
 
 /* One kernel launch of a search: every nonce n = nonce_base + v with v in

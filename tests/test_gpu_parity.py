@@ -159,3 +159,16 @@ def test_device_list_context(oracle):
     with Context(devices=[0]) as c:
         assert c.num_devices() == 1
         assert c.search(b"bradfitz", 0, 9999) == (1419516646206828, 9898)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_combine_modes(mode):
+    """The multi-device combine paths on one GPU: RCCL allgather (ncclCommInitAll
+    over the context's devices + ncclAllGather of the 16-B partial) and plain
+    host copies must both return the C2-window answer."""
+    from distributed_bitcoin_minter_amd import Context
+    with Context(devices=[0]) as c:
+        c.set_combine(mode)
+        for _ in range(2):
+            assert c.search(b"bradfitz", 0, 9999) == (1419516646206828, 9898)
+        assert c.search(b"msg", 0, 2) == (4754799531757243342, 1)
