@@ -68,6 +68,22 @@ def instruction_mix_ceiling(p, nbv=1, clock_ghz=2.37):
             "clock_ghz": clock_ghz, "GHs_per_gpu": round(ghs, 2)}
 
 
+def pmc_traffic(p, nbv=1):
+    """HBM bytes per launch of search_kernel<p, nbv> from the newest committed
+    rocprofv3 PMC summary (FETCH_SIZE + WRITE_SIZE passes, tools/pmc_summary.py);
+    PMC passes cannot run inside this timed process."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), reverse=True):
+        try:
+            summ = json.load(open(path))
+        except ValueError:
+            continue
+        for k, e in summ.items():
+            if f"search_kernel<{p}, {nbv}>" in k and "hbm_bytes_per_launch" in e:
+                return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(target_s=10.0):
     """Time the oracle loop (test infrastructure: the CPU 'port' of
     hash.go + miner.go) on this host over a bounded sample of C2."""
@@ -156,6 +172,7 @@ def main():
     C = compressions_per_nonce(len(MSG), dom_digits)
     achieved = dom_nonces * C * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
     mix = instruction_mix_ceiling(dom_p)
+    traffic, traffic_src = pmc_traffic(dom_p)
     check = None
     if world == 1:
         check = list(res)  # C2 golden: (5256245051, 1626825724)
@@ -178,7 +195,8 @@ def main():
                    "msg": MSG.decode(), "nonces_per_gpu": PER_GPU, "global_nonces": PER_GPU * world,
                    "parallelism": f"range-split x{world}" + (", RCCL all_gather of 16 B partials" if world > 1 else "")},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_T, 2),
-                     "unit": "T int32 lane-ops/s", "frac": round(achieved / VALU_PEAK_T, 4), "traffic": None,
+                     "unit": "T int32 lane-ops/s", "frac": round(achieved / VALU_PEAK_T, 4), "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE+WRITE_SIZE)", "traffic_src": traffic_src,
                      "kernel": f"search_kernel<P={dom_p},NBV=1> ({dom_digits}-digit nonces)",
                      "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom_nonces,
                      "ops_per_nonce": C * OPS_PER_COMPRESSION, "grid": dom_grid,

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (gpurun_out/pmc_*/..._counter_collection.csv)
+into profiles/<round>/pmc_summary.json, per kernel: counters summed per
+dispatch and averaged over dispatches, HBM bytes per launch
+(FETCH_SIZE + WRITE_SIZE, KB -> bytes; MI355X_MICROARCH.md §HBM), the
+effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration) and VALU issue rate.
+Usage: pmc_summary.py <out_dir> [gpurun_out]"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+out_dir = sys.argv[1]
+src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out"
+per = collections.defaultdict(lambda: collections.defaultdict(dict))  # kernel -> dispatch -> counter
+dur = collections.defaultdict(dict)
+for f in glob.glob(os.path.join(src, "pmc_*", "*_counter_collection.csv")):
+    tag = os.path.basename(os.path.dirname(f))
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"]
+        d = (tag, r["Dispatch_Id"])
+        per[k][d][r["Counter_Name"]] = per[k][d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        dur[k][d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+res = {}
+for k, disp in per.items():
+    if "search_kernel" not in k:
+        continue
+    acc, n = collections.defaultdict(list), collections.Counter()
+    for d, cs in disp.items():
+        for c, v in cs.items():
+            acc[c].append(v)
+        acc["_dur_s"].append(dur[k][d])
+    m = {c: sum(v) / len(v) for c, v in acc.items()}
+    e = {"counters": {c: v for c, v in m.items() if not c.startswith("_")}, "duration_ms": m["_dur_s"] * 1e3}
+    if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+        e["hbm_bytes_per_launch"] = int((m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024)
+    if "GRBM_GUI_ACTIVE" in m:
+        e["clock_ghz"] = m["GRBM_GUI_ACTIVE"] / 8 / m["_dur_s"] / 1e9
+        if "SQ_INSTS_VALU" in m:
+            e["simd_cycles_per_valu"] = (m["GRBM_GUI_ACTIVE"] / 8) * 1024 / m["SQ_INSTS_VALU"]
+    res[k] = e
+os.makedirs(out_dir, exist_ok=True)
+json.dump(res, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
+for k, e in res.items():
+    print(k[:60], {x: (round(y, 3) if isinstance(y, float) else y) for x, y in e.items() if x != "counters"})
