@@ -172,3 +172,18 @@ def test_combine_modes(mode):
         for _ in range(2):
             assert c.search(b"bradfitz", 0, 9999) == (1419516646206828, 9898)
         assert c.search(b"msg", 0, 2) == (4754799531757243342, 1)
+
+
+def test_c4_shape_single_process(gpu_ctx, oracle):
+    """C4's path (one process, every visible GPU, one ctx) at 2^34 nonces:
+    the answer re-hashes to itself, equals the min over two halves, and its
+    neighbourhood re-scanned by the oracle agrees."""
+    from distributed_bitcoin_minter_amd import Context, device_count
+    msg, lo, hi = b"bradfitz", 0, (1 << 34) - 1
+    with Context(num_gpus=device_count()) as c:
+        h, n = c.search(msg, lo, hi)
+    assert gpu_ctx.hash_many(msg, [n]) == [h]
+    mid = (1 << 33) - 1
+    assert min(gpu_ctx.search(msg, lo, mid), gpu_ctx.search(msg, mid + 1, hi)) == (h, n)
+    a, b = max(lo, n - 20000), min(hi, n + 20000)
+    assert oracle.search(msg, a, b, threads=8) == (h, n)
