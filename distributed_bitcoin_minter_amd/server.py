@@ -1,0 +1,257 @@
+"""Bitcoin server: the range scheduler between request clients and miners.
+
+Reference: project2/bitcoin/server/server.go (``acceptMessage`` :73-142,
+``scheduleJobs`` :145-197, ``minerLoad = 24`` :18) and the Part B spec,
+project2/README.md:341-417.  The reference does not compile;
+this module implements the behaviour the spec asks for, over the same wire
+format (JSON ``bitcoin.Message`` inside LSP payloads):
+
+* A miner connects and sends ``Join`` (README:376); it is then idle.
+* A client sends ``Request(Data, Lower, Upper)`` (README:382-385).  The server
+  cuts ``[Lower, Upper]`` (inclusive, README:329) into chunks of ``chunk``
+  nonces and hands them to idle miners as ``Request`` messages.
+* Each miner answers ``Result(Hash, Nonce)``; when every chunk of a request
+  is back, the client gets ``Result`` with the minimum (README:392-393).
+
+Differences from server.go, each deliberate:
+
+* Chunk size.  ``minerLoad = 24`` (:18) makes a GPU miner spend all its time
+  in the protocol; the default here is 2^32 nonces (about 0.13 s on one
+  MI355X), the retune SURVEY.md §8f(f1) asks for.  (:157-169 also lose the
+  intended ``upper = lower + 24`` to ``:=`` shadowing; chunks here tile the
+  range exactly.)
+* Merge.  server.go:113 keeps the first strict-``<`` result in ARRIVAL order,
+  so a hash tie between two chunks resolves differently run to run.  Here
+  the merge is the lexicographic (hash, nonce) minimum, which equals the
+  sequential strict-``<`` scan of the whole range whatever
+  order the chunks come back in.
+* Failures (README:408-417, absent from server.go but for :177-179).  A lost
+  miner's chunk goes back to the front of its request's queue and is handed
+  to the next idle miner (or waits for one to join).  A lost client's request
+  is dropped; chunks already on miners finish and their results are ignored.
+
+Scheduler (README:417 asks for it to be documented): fair share by
+assignment count.  Whenever a miner is idle, it gets the next chunk of the
+active request that currently has the FEWEST chunks in flight, ties going to
+the oldest request.  With m miners and r requests each request therefore
+holds floor(m/r) or ceil(m/r) miners at any moment, and a new request gets
+miners as soon as the next ones free up instead of waiting for earlier
+requests to drain.  Chunks of one request are issued in ascending order.
+
+The server is one event loop on one thread (the LSP endpoint has its own
+reader/epoch threads): every decision happens in ``_on_message`` /
+``_on_lost``, so there are no locks in the scheduler itself.
+"""
+import argparse
+import collections
+import itertools
+import sys
+
+from . import lsp
+from .bitcoin import Message, MsgType, NewRequest, NewResult, U64_MAX
+
+DEFAULT_CHUNK = 1 << 32
+
+
+class _Request:
+    """One client request being mined."""
+    __slots__ = ("rid", "client", "data", "lower", "upper", "next_lower", "done", "retry",
+                 "inflight", "best", "answered")
+
+    def __init__(self, rid, client, msg):
+        self.rid = rid
+        self.client = client
+        self.data = msg.Data
+        self.lower = msg.Lower
+        self.upper = msg.Upper
+        self.next_lower = msg.Lower        # first nonce not yet handed out
+        self.done = msg.Lower > msg.Upper  # every chunk issued
+        self.retry = collections.deque()   # chunks of lost miners, issued first
+        self.inflight = 0
+        self.best = (U64_MAX, U64_MAX)     # miner.go:45-46 initial state
+        self.answered = False
+
+    def has_work(self):
+        return bool(self.retry) or not self.done
+
+    def finished(self):
+        return not self.has_work() and self.inflight == 0
+
+    def take(self, chunk):
+        """Next chunk [lo, hi] (inclusive)."""
+        if self.retry:
+            return self.retry.popleft()
+        lo = self.next_lower
+        hi = lo + chunk - 1 if self.upper - lo >= chunk else self.upper
+        if hi == self.upper:
+            self.done = True
+        else:
+            self.next_lower = hi + 1
+        return lo, hi
+
+    def merge(self, h, n):
+        if (h, n) < self.best:
+            self.best = (h, n)
+
+
+class BitcoinServer:
+    """Owns an ``lsp.Server``; ``serve()`` runs the event loop until the LSP
+    server is closed (``close()`` from another thread ends it)."""
+
+    def __init__(self, lsp_server, chunk=DEFAULT_CHUNK, log=None):
+        if chunk < 1:
+            raise ValueError("chunk must be >= 1")
+        self.srv = lsp_server
+        self.chunk = int(chunk)
+        self.log = log or (lambda *a: None)
+        self.miners = {}                    # conn id -> (request id, lo, hi) or None when idle
+        self.idle = collections.deque()     # idle miner ids, FIFO
+        self.requests = collections.OrderedDict()  # rid -> _Request, oldest first
+        self.client_reqs = collections.defaultdict(collections.deque)  # client -> rids, in arrival order
+        self._rids = itertools.count(1)
+        self.stats = collections.Counter()
+
+    # ---- event handling -------------------------------------------------
+    def serve(self):
+        while True:
+            try:
+                cid, payload = self.srv.Read()
+            except lsp.LSPError as e:
+                if e.conn_id == 0:
+                    return  # server closed
+                self._on_lost(e.conn_id)
+                continue
+            try:
+                msg = Message.unmarshal(payload)
+            except (ValueError, KeyError, TypeError):
+                self.log(f"conn {cid}: bad message {payload!r}")
+                continue
+            self._on_message(cid, msg)
+
+    def _on_message(self, cid, msg):
+        if msg.Type == MsgType.Join:
+            if cid not in self.miners:
+                self.miners[cid] = None
+                self.idle.append(cid)
+                self.stats["joins"] += 1
+        elif msg.Type == MsgType.Request:
+            if cid in self.miners:
+                return  # a miner does not make requests
+            r = _Request(next(self._rids), cid, msg)
+            self.requests[r.rid] = r
+            self.client_reqs[cid].append(r.rid)
+            self.stats["requests"] += 1
+            self._maybe_finish(r)
+        elif msg.Type == MsgType.Result:
+            job = self.miners.get(cid)
+            if job is None:
+                return  # not a miner, or a miner with no job: stray
+            rid, lo, hi = job
+            self.miners[cid] = None
+            self.idle.append(cid)
+            r = self.requests.get(rid)
+            if r is not None:  # None: its client is gone, ignore (README:414)
+                r.inflight -= 1
+                r.merge(msg.Hash, msg.Nonce)
+                self.stats["chunks_done"] += 1
+                self._maybe_finish(r)
+        self._schedule()
+
+    def _on_lost(self, cid):
+        if cid in self.miners:
+            job = self.miners.pop(cid)
+            try:
+                self.idle.remove(cid)
+            except ValueError:
+                pass
+            self.stats["miners_lost"] += 1
+            if job is not None:
+                rid, lo, hi = job
+                r = self.requests.get(rid)
+                if r is not None:
+                    r.inflight -= 1
+                    r.retry.appendleft((lo, hi))  # README:413: reassign
+                    self.stats["chunks_reassigned"] += 1
+        elif cid in self.client_reqs:
+            for rid in self.client_reqs.pop(cid):
+                self.requests.pop(rid, None)  # README:414: stop working for it
+            self.stats["clients_lost"] += 1
+        self._schedule()
+
+    # ---- scheduling -----------------------------------------------------
+    def _pick(self):
+        """Active request with the fewest chunks in flight (oldest on ties)."""
+        best = None
+        for r in self.requests.values():
+            if r.has_work() and (best is None or r.inflight < best.inflight):
+                best = r
+        return best
+
+    def _schedule(self):
+        while self.idle:
+            r = self._pick()
+            if r is None:
+                return
+            mid = self.idle.popleft()
+            lo, hi = r.take(self.chunk)
+            try:
+                self.srv.Write(mid, NewRequest(r.data, lo, hi).marshal())
+            except lsp.LSPError:
+                # miner already gone (server.go:177-179): put the chunk back
+                self.miners.pop(mid, None)
+                r.retry.appendleft((lo, hi))
+                continue
+            self.miners[mid] = (r.rid, lo, hi)
+            r.inflight += 1
+            self.stats["chunks_sent"] += 1
+
+    def _maybe_finish(self, r):
+        if not r.finished():
+            return
+        r.answered = True
+        q = self.client_reqs.get(r.client)
+        # answer a client's requests in the order it sent them
+        while q and self.requests[q[0]].answered:
+            done = self.requests.pop(q.popleft())
+            try:
+                self.srv.Write(done.client, NewResult(*done.best).marshal())
+                self.stats["results"] += 1
+            except lsp.LSPError:
+                pass  # client gone; its loss is reported by Read
+        if q is not None and not q:
+            self.client_reqs.pop(r.client, None)
+
+    def close(self):
+        try:
+            self.srv.Close()
+        except lsp.LSPError:
+            pass
+
+
+def main(argv=None):
+    """``server <port>`` (README:365-368)."""
+    ap = argparse.ArgumentParser(prog="server", description="bitcoin mining server (LSP)")
+    ap.add_argument("port", type=int)
+    ap.add_argument("--chunk", type=int, default=DEFAULT_CHUNK, help="nonces per miner job (default 2^32)")
+    ap.add_argument("--epoch-limit", type=int, default=lsp.DefaultEpochLimit)
+    ap.add_argument("--epoch-millis", type=int, default=lsp.DefaultEpochMillis)
+    ap.add_argument("--window-size", type=int, default=lsp.DefaultWindowSize)
+    ap.add_argument("-v", action="store_true", help="log to stderr")
+    a = ap.parse_args(argv)
+    params = lsp.Params(a.epoch_limit, a.epoch_millis, a.window_size)
+    try:
+        srv = lsp.NewServer(a.port, params)
+    except lsp.LSPError as e:
+        print(f"Failed to start server: {e}", file=sys.stderr)
+        return 1
+    log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if a.v else None
+    s = BitcoinServer(srv, chunk=a.chunk, log=log)
+    try:
+        s.serve()
+    except KeyboardInterrupt:
+        s.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

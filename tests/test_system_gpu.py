@@ -1,0 +1,110 @@
+"""The whole system with GPU miners: LSP server + GPU miner processes
+(miner.run over libbtcminer.so) + request clients (BASELINE configs C1 and
+C5 on one MI355X).  Each miner owns its own bm_ctx; on a one-GPU box all of
+them share device 0 (their launches run on separate streams).
+
+Parity: every client's answer equals one whole-range bm_search_gpu call and,
+for the oracle-sized cases, the CPU oracle's sequential scan.
+"""
+import io
+import threading
+import time
+
+import pytest
+
+from distributed_bitcoin_minter_amd import Miner, client, device_count, lsp, lspnet, miner
+from distributed_bitcoin_minter_amd.server import BitcoinServer
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _reset_drops():
+    lspnet.ResetDropPercent()
+    lspnet.seed(0x5EED)
+    yield
+    lspnet.ResetDropPercent()
+
+
+def start(chunk, p, nminers):
+    srv = lsp.NewServer(0, p)
+    bs = BitcoinServer(srv, chunk=chunk)
+    threads = [threading.Thread(target=bs.serve, daemon=True)]
+    ndev = max(1, device_count())
+    gminers = [Miner(devices=[i % ndev]) for i in range(nminers)]
+    for m in gminers:
+        threads.append(threading.Thread(target=miner.run, args=(f"127.0.0.1:{srv.port}", p),
+                                        kwargs={"searcher": m}, daemon=True))
+    for t in threads:
+        t.start()
+    t0 = time.monotonic()
+    while bs.stats["joins"] < nminers:
+        assert time.monotonic() - t0 < 30
+        time.sleep(0.01)
+    return srv, bs, threads, gminers
+
+
+def stop(bs, threads, gminers):
+    lspnet.ResetDropPercent()
+    bs.close()
+    for t in threads:
+        t.join(timeout=15)
+    for m in gminers:
+        m.close()
+
+
+def test_c1_gpu_miner_end_to_end():
+    p = lsp.Params(EpochLimit=50, EpochMillis=20, WindowSize=1)
+    srv, bs, threads, gm = start(1000, p, 1)
+    out = io.StringIO()
+    client.main([f"127.0.0.1:{srv.port}", "bradfitz", "9999", "--epoch-millis", "20", "--epoch-limit", "50"], out=out)
+    assert out.getvalue() == "Result 1419516646206828 9898\n"
+    stop(bs, threads, gm)
+
+
+def test_c5_gpu_miners_16_clients_10pct_drop(gpu_ctx, oracle):
+    p = lsp.Params(EpochLimit=200, EpochMillis=20, WindowSize=1)
+    srv, bs, threads, gm = start(1 << 24, p, 4)
+    lspnet.SetReadDropPercent(10)
+    lspnet.SetWriteDropPercent(10)
+    msgs = [f"client-{i:02d}" for i in range(16)]
+    tops = [(1 << 28) - 1 - 9973 * i for i in range(16)]
+    got = {}
+
+    def ask(i):
+        got[i] = client.request(f"127.0.0.1:{srv.port}", msgs[i], tops[i], p)
+
+    th = [threading.Thread(target=ask, args=(i,)) for i in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    lspnet.ResetDropPercent()
+    for i in range(16):
+        assert got.get(i) == gpu_ctx.search(msgs[i].encode(), 0, tops[i]), i
+    for i in (0, 15):
+        assert got[i] == oracle.search(msgs[i].encode(), 0, tops[i], threads=8), i
+    assert bs.stats["chunks_done"] >= 16 * 16
+    stop(bs, threads, gm)
+
+
+def test_gpu_miner_failover():
+    """A GPU miner dies mid-request; its chunk is redone by another."""
+    p = lsp.Params(EpochLimit=5, EpochMillis=20, WindowSize=1)
+    srv, bs, threads, gm = start(1 << 26, p, 2)
+    victim = gm[0]
+    orig = victim.search
+    calls = []
+
+    def crash_once(data, lo, hi):
+        calls.append((lo, hi))
+        if len(calls) == 1:
+            raise RuntimeError("miner process died")
+        return orig(data, lo, hi)
+
+    victim.search = crash_once
+    res = client.request(f"127.0.0.1:{srv.port}", "bradfitz", (1 << 29) - 1, p)
+    with Miner() as ref:
+        assert res == ref.search("bradfitz", 0, (1 << 29) - 1)
+    assert bs.stats["miners_lost"] == 1 and bs.stats["chunks_reassigned"] == 1
+    stop(bs, threads, gm)
