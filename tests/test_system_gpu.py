@@ -32,9 +32,14 @@ def start(chunk, p, nminers):
     threads = [threading.Thread(target=bs.serve, daemon=True)]
     ndev = max(1, device_count())
     gminers = [Miner(devices=[i % ndev]) for i in range(nminers)]
+    def run(m):
+        try:
+            miner.run(f"127.0.0.1:{srv.port}", p, searcher=m)
+        except RuntimeError:
+            pass  # test_gpu_miner_failover's victim: the miner process dies
+
     for m in gminers:
-        threads.append(threading.Thread(target=miner.run, args=(f"127.0.0.1:{srv.port}", p),
-                                        kwargs={"searcher": m}, daemon=True))
+        threads.append(threading.Thread(target=run, args=(m,), daemon=True))
     for t in threads:
         t.start()
     t0 = time.monotonic()
