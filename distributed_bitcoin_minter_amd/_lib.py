@@ -85,6 +85,7 @@ def load():
         "bm_ctx_set_blocks_per_cu": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_ctx_set_max_windows": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_ctx_set_combine": ([vp, ctypes.c_int], ctypes.c_int),
+        "bm_ctx_set_task_digits": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_plan_segments": ([ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, P(Segment), ctypes.c_int,
                               P(ctypes.c_int)], ctypes.c_int),
         "bm_plan_segments_ex": ([ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, ctypes.c_int, P(Segment),
@@ -190,6 +191,9 @@ class Context:
 
     def set_combine(self, mode: int):
         check(self._lib.bm_ctx_set_combine(self.handle, mode), "bm_ctx_set_combine")
+
+    def set_task_digits(self, digits: int):
+        check(self._lib.bm_ctx_set_task_digits(self.handle, digits), "bm_ctx_set_task_digits")
 
     def set_max_windows(self, n: int):
         check(self._lib.bm_ctx_set_max_windows(self.handle, n), "bm_ctx_set_max_windows")

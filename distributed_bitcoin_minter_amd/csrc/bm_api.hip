@@ -81,6 +81,7 @@ struct bm_ctx {
     int blocks_per_cu = 0;
     int max_windows = bm::kDefaultMaxWindows;
     int combine = BM_COMBINE_AUTO;
+    int task_digits = 0;  // 0: per launch (size_launch); 1 or 2: forced
     bool nccl_ready = false;
     bm_stats_t stats;
 };
@@ -112,12 +113,27 @@ int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_
     // word LW holds one digit: the kernel steps the next one in word LW-1
     // (bm_kernels.hpp TWOW), so a task can still be 100 nonces
     if (s.p % 4 == 0 && s.p / 4 >= 1 && s.nd >= 2) ms = 2;
+    const uint64_t resident = (uint64_t)blocks_per_cu(ctx, d, fn) * (uint64_t)d.cus;
+    if (ctx->task_digits > 0) {
+        ms = std::min(ms, ctx->task_digits);
+    } else if (ms > 1) {
+        // A launch with fewer 100-nonce tasks than twice its resident lanes
+        // (the 1..8-digit segments of a search from 0) leaves SIMDs half
+        // empty while each lane runs its one 100-nonce task: use 10-nonce
+        // tasks instead, so every lane has work and the launch ends sooner.
+        const uint64_t lanes = resident * (uint64_t)kBlock;
+        const uint64_t tasks100 = (s.vhi - s.vlo) / 100 + 1;
+        if (tasks100 < 2 * lanes) ms = 1;
+    }
     const uint64_t S = kPow10[ms];
-    const uint32_t m = (uint32_t)std::max<uint64_t>(1, kNoncesPerLaneChunk / S);
     const uint64_t t0 = s.vlo / S, t_end = s.vhi / S + 1;
     const uint64_t T = t_end - t0;
+    // Tasks per lane per dequeue: about 100 nonces, but at least ~8 dequeues
+    // per resident lane so the launch drains evenly (small launches: 1).
+    const uint64_t m_max = std::max<uint64_t>(1, kNoncesPerLaneChunk / S);
+    const uint32_t m = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(m_max, T / (8 * resident * (uint64_t)kBlock)));
     const uint64_t chunks = (T + 64ull * m - 1) / (64ull * m);
-    const uint64_t resident = (uint64_t)blocks_per_cu(ctx, d, fn) * (uint64_t)d.cus;
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, resident));
     const uint64_t k = (chunks + grid * 4 - 1) / (grid * 4);  // chunks per wave (approx.)
 
@@ -494,6 +510,12 @@ int bm_ctx_set_blocks_per_cu(bm_ctx_t* ctx, int blocks_per_cu) {
 int bm_ctx_set_combine(bm_ctx_t* ctx, int mode) {
     if (!ctx || mode < BM_COMBINE_AUTO || mode > BM_COMBINE_HOST) return BM_EINVAL;
     ctx->combine = mode;
+    return BM_OK;
+}
+
+int bm_ctx_set_task_digits(bm_ctx_t* ctx, int digits) {
+    if (!ctx || digits < 0 || digits > bm::kMaxInnerDigits) return BM_EINVAL;
+    ctx->task_digits = digits;
     return BM_OK;
 }
 

@@ -129,6 +129,13 @@ int bm_ctx_set_blocks_per_cu(bm_ctx_t* ctx, int blocks_per_cu);
  * Results do not depend on it. */
 int bm_ctx_set_max_windows(bm_ctx_t* ctx, int max_windows);
 
+/* Nonces per kernel task = 10^digits, the digits a lane steps in its inner
+ * loop.  0 (default): per launch, 100-nonce tasks, or 10-nonce tasks for a
+ * launch too small to give every resident lane two 100-nonce tasks; 1 or 2:
+ * forced (tests use it to cover both loop shapes at small sizes).  Results do
+ * not depend on it. */
+int bm_ctx_set_task_digits(bm_ctx_t* ctx, int digits);
+
 /* How a context combines its per-device 16-byte partials:
  * BM_COMBINE_AUTO (default): RCCL allgather when the context has > 1 device,
  * a plain device-to-host copy otherwise; BM_COMBINE_RCCL: always RCCL (also

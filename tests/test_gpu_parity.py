@@ -82,19 +82,26 @@ def test_layout_table_complete():
 
 @pytest.mark.parametrize("key", sorted(_LAYOUTS))
 def test_every_kernel_layout(gpu_ctx, oracle, key):
+    """Each layout with both task shapes: 10-nonce tasks (what a small launch
+    gets by default) and 100-nonce tasks (forced; large launches' default)."""
     msg, lo, hi, mw = _LAYOUTS[key]
+    want = oracle.search(msg, lo, hi, threads=8)
     gpu_ctx.set_max_windows(mw)
     try:
-        assert gpu_ctx.search(msg, lo, hi) == oracle.search(msg, lo, hi, threads=8)
-        st = gpu_ctx.last_stats()
-        assert any((st.launch[i].nbv, st.launch[i].p) == key for i in range(st.recorded))
+        for td in (0, 2):
+            gpu_ctx.set_task_digits(td)
+            assert gpu_ctx.search(msg, lo, hi) == want, td
+            st = gpu_ctx.last_stats()
+            assert any((st.launch[i].nbv, st.launch[i].p) == key for i in range(st.recorded))
     finally:
         gpu_ctx.set_max_windows(64)
+        gpu_ctx.set_task_digits(0)
 
 
 def test_random_windows(gpu_ctx, oracle):
     rng = random.Random(0x5EED)
-    for _ in range(40):
+    for k in range(40):
+        gpu_ctx.set_task_digits(2 if k % 2 else 0)
         L = rng.choice([0, 3, 8, 20, 45, 54, 55, 60, 63, 64, 100, 120, 128, 250, 600])
         msg = bytes(rng.randrange(32, 127) for _ in range(L))
         D = rng.randint(1, 20)
@@ -103,6 +110,7 @@ def test_random_windows(gpu_ctx, oracle):
         lo = rng.randint(dlo, dhi)
         hi = min(U64, lo + rng.randint(0, 1 << rng.randint(4, 18)))
         assert gpu_ctx.search(msg, lo, hi) == oracle.search(msg, lo, hi, threads=8), (L, lo, hi)
+    gpu_ctx.set_task_digits(0)
 
 
 def test_edges(gpu_ctx, oracle):
