@@ -206,3 +206,60 @@ def test_closeconn_flushes_pending_and_stops_reads():
     assert [c.Read() for _ in range(5)] == [b"m%d" % i for i in range(5)]
     c.Close()
     srv.Close()
+
+
+def test_server_slow_start():
+    """lsp3_test.go ServerSlowStart: a client keeps re-sending Connect each
+    epoch, so a server that starts a few epochs late still gets it."""
+    p = params(ms=30, k=20)
+    probe = lspnet.listen(0)
+    port = probe.local_port()
+    probe.close()
+    got = {}
+    t = threading.Thread(target=lambda: got.setdefault("c", lsp.NewClient(f"127.0.0.1:{port}", p)))
+    t.start()
+    time.sleep(4 * p.EpochMillis / 1000.0)
+    srv = lsp.NewServer(port, p)
+    t.join(timeout=10)
+    c = got["c"]
+    c.Write(b"late")
+    assert srv.Read() == (c.ConnID(), b"late")
+    c.Close()
+    srv.Close()
+
+
+@pytest.mark.parametrize("w", [1, 4])
+def test_network_outage_shorter_than_k_epochs(w):
+    """lsp4_test.go ServerToClient / ClientToServer / RoundTrip: the network
+    drops everything for fewer than K epochs; every message still arrives,
+    in order, once it comes back."""
+    p = params(w=w, ms=20, k=30)
+    srv, stop, t = echo_server(p)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", p)
+    lspnet.SetWriteDropPercent(100)
+    for i in range(12):
+        c.Write(b"m%d" % i)
+    time.sleep(10 * p.EpochMillis / 1000.0)  # 10 epochs of silence < K = 30
+    lspnet.SetWriteDropPercent(0)
+    assert [c.Read() for _ in range(12)] == [b"m%d" % i for i in range(12)]
+    time.sleep(3 * p.EpochMillis / 1000.0)
+    c.Close()
+    stop.set()
+    srv.Close()
+    t.join(timeout=5)
+
+
+def test_server_fast_close_delivers_pending():
+    """lsp4_test.go ServerFastClose: Close right after many Writes still
+    delivers them all (under drops, through epoch resends)."""
+    p = params(w=2, ms=20, k=100)
+    srv = lsp.NewServer(0, p)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", p)
+    cid = c.ConnID()
+    lspnet.SetServerWriteDropPercent(30)
+    for i in range(10):
+        srv.Write(cid, b"s%d" % i)
+    srv.Close()  # blocks until the client has acknowledged all 10
+    lspnet.SetServerWriteDropPercent(0)
+    assert [c.Read() for _ in range(10)] == [b"s%d" % i for i in range(10)]
+    c.Close()
