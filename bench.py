@@ -116,6 +116,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N>1 ranks on ONE GPU (every rank uses device 0, gloo combine on CPU): "
+                         "exercises the multi-rank path on a one-GPU box; not a scaling measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,10 +126,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if args.rehearse_one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    cdev = torch.device("cpu") if args.rehearse_one_gpu else dev
 
     lo = rank * PER_GPU
     hi = lo + PER_GPU - 1
@@ -141,7 +150,7 @@ def main():
             L = st.launch[i]
             if dom is None or L.nonces > dom.nonces:
                 dom = L
-        res = combine(part, device=dev) if world > 1 else part
+        res = combine(part, device=cdev) if world > 1 else part
         return res, (dom.nonces, dom.ms, dom.digits, dom.p, dom.grid, dom.tasks_per_thread, dom.inner_digits)
 
     for _ in range(args.warmup):
@@ -161,7 +170,7 @@ def main():
     sync()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = tt.item()
 
@@ -205,6 +214,8 @@ def main():
                                                                   / mix["GHs_per_gpu"], 4))},
         "result": check,
     }
+    if args.rehearse_one_gpu:
+        out["rehearsal"] = "all ranks on device 0, gloo combine: checks the multi-rank path, not a measurement"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
