@@ -80,8 +80,8 @@ def pmc_traffic(p, nbv=1):
             continue
         for k, e in summ.items():
             if f"search_kernel<{p}, {nbv}>" in k and "hbm_bytes_per_launch" in e:
-                return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
-    return None, None
+                return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT), e.get("counters", {})
+    return None, None, {}
 
 
 def cpu_baseline(target_s=10.0):
@@ -181,7 +181,9 @@ def main():
     C = compressions_per_nonce(len(MSG), dom_digits)
     achieved = dom_nonces * C * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
     mix = instruction_mix_ceiling(dom_p)
-    traffic, traffic_src = pmc_traffic(dom_p)
+    traffic, traffic_src, pmc = pmc_traffic(dom_p)
+    # measured VALU per nonce (SQ_INSTS_VALU counts wave-instructions: x64 lanes)
+    valu_pmc = pmc["SQ_INSTS_VALU"] * 64 / dom_nonces if "SQ_INSTS_VALU" in pmc else None
     check = None
     if world == 1:
         check = list(res)  # C2 golden: (5256245051, 1626825724)
@@ -206,6 +208,9 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_T, 2),
                      "unit": "T int32 lane-ops/s", "frac": round(achieved / VALU_PEAK_T, 4), "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE+WRITE_SIZE)", "traffic_src": traffic_src,
+                     "traffic_note": "the per-launch dequeue counter's returning atomics (64-B memory-side "
+                                     "requests); the search reads no input from HBM (DESIGN.md §5)",
+                     "valu_per_nonce_pmc": valu_pmc and round(valu_pmc, 1),
                      "kernel": f"search_kernel<P={dom_p},NBV=1> ({dom_digits}-digit nonces)",
                      "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom_nonces,
                      "ops_per_nonce": C * OPS_PER_COMPRESSION, "grid": dom_grid,
