@@ -351,3 +351,80 @@ def test_lost_client_results_ignored():
     s._on_message(1, NewResult(1, 1))  # result for a dead client: miner goes idle
     assert f.results_for(100) == [] and list(s.idle) == [1]
     assert len(f.jobs_for(1)) == 1
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_scheduler_random_event_sequences(seed):
+    """Random joins, losses, requests, client deaths and out-of-order
+    results against the scheduler (no network).  Invariants: every request
+    whose client survives is answered exactly once, in its client's order,
+    with the lexicographic min over its whole inclusive range; a miner never
+    holds two chunks; no chunk of a live request is lost.  The toy hash has
+    many ties, so the nonce tie-break is exercised."""
+    import random
+
+    rng = random.Random(seed)
+
+    def toy_hash(data, n):
+        return (n * 7 + len(data)) % 13
+
+    def brute(data, lo, hi):
+        return min(((toy_hash(data, n), n) for n in range(lo, hi + 1)), default=(U64, U64))
+
+    f, s = make(rng.choice([1, 3, 7, 50]))
+    next_id = [1]
+    miners, clients = set(), {}
+    expected = {}  # client -> [answers in order]
+
+    def new_id():
+        next_id[0] += 1
+        return next_id[0]
+
+    def deliver(mid):
+        job = s.miners.get(mid)
+        if job is not None:
+            rid, lo, hi = job
+            data = next((r.data for r in s.requests.values() if r.rid == rid), "gone")
+            s._on_message(mid, NewResult(*brute(data, lo, hi)))
+
+    for _ in range(300):
+        ev = rng.random()
+        if ev < 0.15 or not miners:
+            m = new_id()
+            miners.add(m)
+            s._on_message(m, NewJoin())
+        elif ev < 0.35:
+            c = rng.choice(list(clients)) if clients and rng.random() < 0.3 else new_id()
+            lo = rng.randint(0, 200)
+            hi = lo + rng.randint(-2, 150)
+            data = f"d{c}-{lo}"
+            clients.setdefault(c, True)
+            s._on_message(c, NewRequest(data, lo, hi))
+            expected.setdefault(c, []).append(brute(data, lo, hi) if lo <= hi else (U64, U64))
+        elif ev < 0.45 and len(miners) > 1:
+            m = rng.choice(sorted(miners))
+            miners.discard(m)
+            s._on_lost(m)
+        elif ev < 0.5 and clients:
+            c = rng.choice(sorted(clients))
+            del clients[c]
+            expected.pop(c, None)
+            s._on_lost(c)
+        else:
+            busy = [m for m in miners if s.miners.get(m) is not None]
+            if busy:
+                deliver(rng.choice(busy))
+        assert all(m in s.miners for m in s.idle) and len(set(s.idle)) == len(s.idle)
+    # drain: answer every outstanding chunk (a miner must exist)
+    if not miners:
+        m = new_id()
+        miners.add(m)
+        s._on_message(m, NewJoin())
+    for _ in range(100000):
+        busy = [m for m in miners if s.miners.get(m) is not None]
+        if not busy:
+            break
+        deliver(busy[0])
+    assert not s.requests, "requests left unanswered"
+    for c, answers in expected.items():
+        assert f.results_for(c) == answers, c
