@@ -40,3 +40,15 @@ def test_go_html_escaping():
 def test_rejects_out_of_range():
     with pytest.raises(ValueError):
         Message.unmarshal(b'{"Type":1,"Lower":18446744073709551616}')
+
+
+def test_invalid_utf8_becomes_replacement_char_like_go():
+    """Go's encoding/json replaces invalid UTF-8 in a string with U+FFFD, so a
+    Go miner hashes the replacement's bytes.  A Python str
+    holding undecodable argv bytes (surrogateescape) takes the same path."""
+    raw = b"caf\xe9"  # Latin-1 bytes, invalid UTF-8
+    data = raw.decode("utf-8", "surrogateescape")
+    wire = NewRequest(data, 0, 1).marshal()
+    back = Message.unmarshal(wire)
+    assert back.Data == "caf�"
+    assert back.Data.encode() == b"caf\xef\xbf\xbd"
