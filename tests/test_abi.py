@@ -53,3 +53,32 @@ def test_no_gpu_fails_loudly():
     with pytest.raises(_lib.BtcMinerError) as ei:
         _lib.Context(num_gpus=1)
     assert ei.value.status == _lib.BM_ENODEV
+
+
+def _c_client():
+    """examples/bm_c_client: a plain C program using only include/btcminer.h
+    (built by __graft_entry__.build(); rebuilt here if absent)."""
+    import subprocess
+    exe = os.path.join(ROOT, "examples", "bm_c_client")
+    if not os.path.exists(exe):
+        subprocess.check_call(["gcc", "-O2", "-I", os.path.join(ROOT, "include"),
+                               os.path.join(ROOT, "examples", "bm_c_client.c"),
+                               "-L", os.path.join(ROOT, "distributed_bitcoin_minter_amd"), "-lbtcminer",
+                               "-Wl,-rpath,$ORIGIN/../distributed_bitcoin_minter_amd", "-o", exe])
+    return exe
+
+
+@pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")
+def test_c_consumer_links_and_fails_loudly_without_gpu():
+    import subprocess
+    r = subprocess.run([_c_client(), "bradfitz", "0", "9999"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and r.stdout == "error -2 no usable gfx950 device\n"
+
+
+@pytest.mark.gpu
+def test_c_consumer_on_gpu():
+    import subprocess
+    r = subprocess.run([_c_client(), "bradfitz", "0", "9999"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout == "Result 1419516646206828 9898\n", r.stdout + r.stderr
+    r = subprocess.run([_c_client(), "msg", "5", "4"], capture_output=True, text=True, timeout=60)
+    assert r.stdout == "Result 18446744073709551615 18446744073709551615\n"  # empty range, miner.go:45-46
