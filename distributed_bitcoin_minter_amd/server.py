@@ -31,12 +31,21 @@ Differences from server.go, each deliberate:
   is dropped; chunks already on miners finish and their results are ignored.
 
 Scheduler (README:417 asks for it to be documented): fair share by
-assignment count.  Whenever a miner is idle, it gets the next chunk of the
-active request that currently has the FEWEST chunks in flight, ties going to
-the oldest request.  With m miners and r requests each request therefore
-holds floor(m/r) or ceil(m/r) miners at any moment, and a new request gets
-miners as soon as the next ones free up instead of waiting for earlier
-requests to drain.  Chunks of one request are issued in ascending order.
+assignment count.  Whenever a miner has a free job slot, it gets the next
+chunk of the active request that currently has the FEWEST chunks in flight,
+ties going to the oldest request.  With m miners and r requests each request
+therefore holds floor(m/r) or ceil(m/r) of the miners' slots at any moment,
+and a new request gets slots as soon as the next ones free up instead of
+waiting for earlier requests to drain.  Chunks of one request are issued in
+ascending order.
+
+Job queue depth.  Each miner holds up to ``depth`` jobs (default 2; the
+reference's one-job-per-miner is depth 1).  A miner works through its jobs in
+order (LSP delivers in order), so when a GPU finishes a chunk the next one is
+already in its window: it does not idle for the Result -> Request round
+trip, which under packet loss includes a whole LSP epoch (2 s by default)
+per dropped message.  Free slots are filled level by level: every miner gets
+its first job before any gets a second.
 
 The server is one event loop on one thread (the LSP endpoint has its own
 reader/epoch threads): every decision happens in ``_on_message`` /
@@ -51,6 +60,7 @@ from . import lsp
 from .bitcoin import Message, MsgType, NewRequest, NewResult, U64_MAX
 
 DEFAULT_CHUNK = 1 << 32
+DEFAULT_DEPTH = 2
 
 
 class _Request:
@@ -98,18 +108,24 @@ class BitcoinServer:
     """Owns an ``lsp.Server``; ``serve()`` runs the event loop until the LSP
     server is closed (``close()`` from another thread ends it)."""
 
-    def __init__(self, lsp_server, chunk=DEFAULT_CHUNK, log=None):
-        if chunk < 1:
-            raise ValueError("chunk must be >= 1")
+    def __init__(self, lsp_server, chunk=DEFAULT_CHUNK, depth=DEFAULT_DEPTH, log=None):
+        if chunk < 1 or depth < 1:
+            raise ValueError("chunk and depth must be >= 1")
         self.srv = lsp_server
         self.chunk = int(chunk)
+        self.depth = int(depth)
         self.log = log or (lambda *a: None)
-        self.miners = {}                    # conn id -> (request id, lo, hi) or None when idle
-        self.idle = collections.deque()     # idle miner ids, FIFO
+        self.miners = {}                    # conn id -> deque of (request id, lo, hi) sent, oldest first
+        self._free_since = {}               # conn id -> tick at which its job count last dropped
+        self._tick = itertools.count()
         self.requests = collections.OrderedDict()  # rid -> _Request, oldest first
         self.client_reqs = collections.defaultdict(collections.deque)  # client -> rids, in arrival order
         self._rids = itertools.count(1)
         self.stats = collections.Counter()
+
+    def idle_miners(self):
+        """Miners with no job at all."""
+        return [m for m, jobs in self.miners.items() if not jobs]
 
     # ---- event handling -------------------------------------------------
     def serve(self):
@@ -131,8 +147,8 @@ class BitcoinServer:
     def _on_message(self, cid, msg):
         if msg.Type == MsgType.Join:
             if cid not in self.miners:
-                self.miners[cid] = None
-                self.idle.append(cid)
+                self.miners[cid] = collections.deque()
+                self._free_since[cid] = next(self._tick)
                 self.stats["joins"] += 1
         elif msg.Type == MsgType.Request:
             if cid in self.miners:
@@ -143,12 +159,12 @@ class BitcoinServer:
             self.stats["requests"] += 1
             self._maybe_finish(r)
         elif msg.Type == MsgType.Result:
-            job = self.miners.get(cid)
-            if job is None:
+            jobs = self.miners.get(cid)
+            if not jobs:
                 return  # not a miner, or a miner with no job: stray
-            rid, lo, hi = job
-            self.miners[cid] = None
-            self.idle.append(cid)
+            # a miner answers its jobs in the order it got them (LSP delivers in order)
+            rid, lo, hi = jobs.popleft()
+            self._free_since[cid] = next(self._tick)
             r = self.requests.get(rid)
             if r is not None:  # None: its client is gone, ignore (README:414)
                 r.inflight -= 1
@@ -159,18 +175,14 @@ class BitcoinServer:
 
     def _on_lost(self, cid):
         if cid in self.miners:
-            job = self.miners.pop(cid)
-            try:
-                self.idle.remove(cid)
-            except ValueError:
-                pass
+            jobs = self.miners.pop(cid)
+            self._free_since.pop(cid, None)
             self.stats["miners_lost"] += 1
-            if job is not None:
-                rid, lo, hi = job
+            for rid, lo, hi in reversed(jobs):  # README:413: reassign, lowest chunk first
                 r = self.requests.get(rid)
                 if r is not None:
                     r.inflight -= 1
-                    r.retry.appendleft((lo, hi))  # README:413: reassign
+                    r.retry.appendleft((lo, hi))
                     self.stats["chunks_reassigned"] += 1
         elif cid in self.client_reqs:
             for rid in self.client_reqs.pop(cid):
@@ -187,21 +199,35 @@ class BitcoinServer:
                 best = r
         return best
 
+    def _free_miner(self):
+        """Miner with a free job slot: fewest queued jobs first, then the one
+        whose count dropped longest ago."""
+        best, key = None, None
+        for m, jobs in self.miners.items():
+            if len(jobs) < self.depth:
+                k = (len(jobs), self._free_since[m])
+                if key is None or k < key:
+                    best, key = m, k
+        return best
+
     def _schedule(self):
-        while self.idle:
+        while True:
+            mid = self._free_miner()
+            if mid is None:
+                return
             r = self._pick()
             if r is None:
                 return
-            mid = self.idle.popleft()
             lo, hi = r.take(self.chunk)
             try:
                 self.srv.Write(mid, NewRequest(r.data, lo, hi).marshal())
             except lsp.LSPError:
-                # miner already gone (server.go:177-179): put the chunk back
-                self.miners.pop(mid, None)
+                # miner already gone (server.go:177-179): put the chunk back,
+                # and its queued jobs with it
                 r.retry.appendleft((lo, hi))
-                continue
-            self.miners[mid] = (r.rid, lo, hi)
+                self._on_lost(mid)
+                return
+            self.miners[mid].append((r.rid, lo, hi))
             r.inflight += 1
             self.stats["chunks_sent"] += 1
 
@@ -233,6 +259,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser(prog="server", description="bitcoin mining server (LSP)")
     ap.add_argument("port", type=int)
     ap.add_argument("--chunk", type=int, default=DEFAULT_CHUNK, help="nonces per miner job (default 2^32)")
+    ap.add_argument("--depth", type=int, default=DEFAULT_DEPTH,
+                    help="jobs queued per miner (default 2: the next job is already there when one ends)")
     ap.add_argument("--epoch-limit", type=int, default=lsp.DefaultEpochLimit)
     ap.add_argument("--epoch-millis", type=int, default=lsp.DefaultEpochMillis)
     ap.add_argument("--window-size", type=int, default=lsp.DefaultWindowSize)
@@ -245,7 +273,7 @@ def main(argv=None):
         print(f"Failed to start server: {e}", file=sys.stderr)
         return 1
     log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if a.v else None
-    s = BitcoinServer(srv, chunk=a.chunk, log=log)
+    s = BitcoinServer(srv, chunk=a.chunk, depth=a.depth, log=log)
     try:
         s.serve()
     except KeyboardInterrupt:

@@ -13,6 +13,7 @@ The miners here search with the CPU oracle (test infrastructure) instead of
 the GPU: these tests pin the control plane; tests/test_system_gpu.py runs
 the same system with GPU miners.
 """
+import collections
 import io
 import threading
 import time
@@ -149,7 +150,7 @@ def test_lost_miner_job_is_reassigned_to_a_later_miner(oracle):
     t = threading.Thread(target=lambda: res.setdefault("r", client.request(s.hostport, "bradfitz", 1999, p)))
     t.start()
     s.wait(lambda: s.bs.stats["miners_lost"] == 1)
-    assert s.bs.stats["chunks_reassigned"] == 1
+    assert s.bs.stats["chunks_reassigned"] == 2  # both queued jobs (depth 2)
     healthy = OracleSearcher(oracle)
     s.add_miner(healthy)
     t.join(timeout=60)
@@ -176,7 +177,7 @@ def test_lost_client_request_is_dropped(oracle):
     s.wait(lambda: s.bs.stats["clients_lost"] == 1)
     sent = s.bs.stats["chunks_sent"]
     assert client.request(s.hostport, "bradfitz", 999, p) == oracle.search(b"bradfitz", 0, 999)
-    assert s.bs.stats["chunks_sent"] - sent <= 10 + 1  # only the new request's chunks (+1 in flight)
+    assert s.bs.stats["chunks_sent"] - sent <= 10 + 2  # only the new request's chunks (+ the doomed queue)
     s.close()
 
 
@@ -250,9 +251,9 @@ class FakeLSP:
         return [(m.Hash, m.Nonce) for c, m in self.sent if c == cid and m.Type == MsgType.Result]
 
 
-def make(chunk):
+def make(chunk, depth=1):
     f = FakeLSP()
-    return f, BitcoinServer(f, chunk=chunk)
+    return f, BitcoinServer(f, chunk=chunk, depth=depth)
 
 
 def test_chunks_tile_the_range_exactly():
@@ -349,7 +350,7 @@ def test_lost_client_results_ignored():
     s._on_message(100, NewRequest("a", 0, 99))
     s._on_lost(100)
     s._on_message(1, NewResult(1, 1))  # result for a dead client: miner goes idle
-    assert f.results_for(100) == [] and list(s.idle) == [1]
+    assert f.results_for(100) == [] and s.idle_miners() == [1]
     assert len(f.jobs_for(1)) == 1
 
 
@@ -371,7 +372,7 @@ def test_scheduler_random_event_sequences(seed):
     def brute(data, lo, hi):
         return min(((toy_hash(data, n), n) for n in range(lo, hi + 1)), default=(U64, U64))
 
-    f, s = make(rng.choice([1, 3, 7, 50]))
+    f, s = make(rng.choice([1, 3, 7, 50]), depth=rng.choice([1, 2, 3]))
     next_id = [1]
     miners, clients = set(), {}
     expected = {}  # client -> [answers in order]
@@ -381,9 +382,9 @@ def test_scheduler_random_event_sequences(seed):
         return next_id[0]
 
     def deliver(mid):
-        job = s.miners.get(mid)
-        if job is not None:
-            rid, lo, hi = job
+        jobs = s.miners.get(mid)
+        if jobs:
+            rid, lo, hi = jobs[0]
             data = next((r.data for r in s.requests.values() if r.rid == rid), "gone")
             s._on_message(mid, NewResult(*brute(data, lo, hi)))
 
@@ -411,20 +412,42 @@ def test_scheduler_random_event_sequences(seed):
             expected.pop(c, None)
             s._on_lost(c)
         else:
-            busy = [m for m in miners if s.miners.get(m) is not None]
+            busy = [m for m in miners if s.miners.get(m)]
             if busy:
                 deliver(rng.choice(busy))
-        assert all(m in s.miners for m in s.idle) and len(set(s.idle)) == len(s.idle)
+        assert all(len(j) <= s.depth for j in s.miners.values())
     # drain: answer every outstanding chunk (a miner must exist)
     if not miners:
         m = new_id()
         miners.add(m)
         s._on_message(m, NewJoin())
     for _ in range(100000):
-        busy = [m for m in miners if s.miners.get(m) is not None]
+        busy = [m for m in miners if s.miners.get(m)]
         if not busy:
             break
         deliver(busy[0])
     assert not s.requests, "requests left unanswered"
     for c, answers in expected.items():
         assert f.results_for(c) == answers, c
+
+
+def test_depth_two_queues_the_next_job():
+    """With depth 2 every miner holds its next chunk before finishing the
+    current one; slots fill level by level and a lost miner's whole queue
+    is reassigned in ascending order."""
+    f, s = make(10, depth=2)
+    s._on_message(1, NewJoin())
+    s._on_message(2, NewJoin())
+    s._on_message(100, NewRequest("x", 0, 59))
+    assert f.jobs_for(1) == [(0, 9), (20, 29)] and f.jobs_for(2) == [(10, 19), (30, 39)]
+    s._on_message(1, NewResult(5, 5))      # answers its oldest job first
+    assert f.jobs_for(1)[-1] == (40, 49)
+    s._on_lost(2)                          # (10,19) and (30,39) go back, lowest first
+    assert list(s.requests.values())[0].retry == collections.deque([(10, 19), (30, 39)])
+    s._on_message(3, NewJoin())
+    assert f.jobs_for(3) == [(10, 19), (30, 39)]
+    for m, jobs in ((1, [(20, 29), (40, 49)]), (3, [(10, 19), (30, 39)])):
+        for lo, hi in jobs:
+            s._on_message(m, NewResult(lo + 1, lo))
+    s._on_message(1, NewResult(99, 50))    # (50, 59) went to miner 1 when it freed up
+    assert f.results_for(100) == [(5, 5)]

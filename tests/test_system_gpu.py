@@ -111,7 +111,7 @@ def test_gpu_miner_failover():
     res = client.request(f"127.0.0.1:{srv.port}", "bradfitz", (1 << 29) - 1, p)
     with Miner() as ref:
         assert res == ref.search("bradfitz", 0, (1 << 29) - 1)
-    assert bs.stats["miners_lost"] == 1 and bs.stats["chunks_reassigned"] == 1
+    assert bs.stats["miners_lost"] == 1 and bs.stats["chunks_reassigned"] >= 1
     stop(bs, threads, gm)
 
 

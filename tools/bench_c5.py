@@ -3,7 +3,7 @@
 lspnet 10% packet drop (read and write, every endpoint).
 
     python tools/bench_c5.py [--max-nonce-bits 34] [--chunk-bits 32] [--miners 4]
-                             [--clients 16] [--drop 10] [--epoch-ms 50]
+                             [--clients 16] [--drop 10] [--epoch-ms 50] [--depth 2] [--window 1]
 
 Client i asks for msg "client-%02d" over [0, 2^bits - 1].  The server cuts
 every request into 2^chunk_bits-nonce jobs and spreads them
@@ -38,13 +38,15 @@ def main():
     ap.add_argument("--drop", type=int, default=10)
     ap.add_argument("--epoch-ms", type=int, default=50)
     ap.add_argument("--epoch-limit", type=int, default=100)
+    ap.add_argument("--depth", type=int, default=2, help="jobs queued per miner (server.DEFAULT_DEPTH)")
+    ap.add_argument("--window", type=int, default=1, help="LSP WindowSize (params.go default 1)")
     a = ap.parse_args()
 
     ndev = max(1, device_count())
-    p = lsp.Params(EpochLimit=a.epoch_limit, EpochMillis=a.epoch_ms, WindowSize=1)
+    p = lsp.Params(EpochLimit=a.epoch_limit, EpochMillis=a.epoch_ms, WindowSize=a.window)
     lspnet.seed(0x5EED)
     srv = lsp.NewServer(0, p)
-    bs = BitcoinServer(srv, chunk=1 << a.chunk_bits)
+    bs = BitcoinServer(srv, chunk=1 << a.chunk_bits, depth=a.depth)
     hostport = f"127.0.0.1:{srv.port}"
     threads = [threading.Thread(target=bs.serve, daemon=True)]
     gminers = [Miner(devices=[i % ndev]) for i in range(a.miners)]
@@ -80,7 +82,7 @@ def main():
 
     total = a.clients * (top + 1)
     out = {"config": "C5", "clients": a.clients, "miners": a.miners, "gpus": ndev, "drop_pct": a.drop,
-           "epoch_ms": a.epoch_ms, "max_nonce": top, "chunk": 1 << a.chunk_bits, "seconds": round(wall, 3),
+           "epoch_ms": a.epoch_ms, "window": a.window, "depth": a.depth, "max_nonce": top, "chunk": 1 << a.chunk_bits, "seconds": round(wall, 3),
            "GHs": round(total / wall / 1e9, 3), "server_stats": stats,
            "all_answered": all(got.get(i) is not None for i in range(a.clients))}
     with Context(devices=list(range(min(ndev, a.miners)))) as ctx:
