@@ -113,6 +113,43 @@ BM_DEV void sha_rounds(uint32_t (&s)[8], uint32_t (&w)[16]) {
     });
 }
 
+// sigma0 in plain shifts, for wave-uniform arguments (the compiler keeps it
+// on the scalar unit).
+BM_DEV uint32_t ssig0_uniform(uint32_t x) {
+    return ((x >> 7) | (x << 25)) ^ ((x >> 18) | (x << 14)) ^ (x >> 3);
+}
+
+// Inner-loop rounds [R0, 64) of the last block, with two shortcuts
+// (BM_FOLD, A/B-able):
+//  * sigma0(W[V]) enters W[V+15]; V is the word that varies per nonce.  There
+//    W[V] = wl + J with disjoint bits (J only fills the low nibbles of '0'
+//    digit bytes), and sigma0 is linear over GF(2), so sigma0(W[V]) =
+//    sigma0(wl) ^ sigma0(J): a per-task value (hoisted) ^ a wave-uniform one
+//    (scalar unit).  s0v is that xor.
+//  * round 63 folds the midstate word `h0_add` into its K constant, so the 'a'
+//    it produces is H0 = st[0] + a64 itself (e64 is never needed).
+// Returns H0; s is left as it entered round 63, so s[1] = a63 (H1 - st[1]).
+template <int R0, int V>
+BM_DEV uint32_t sha_rounds_h0(uint32_t (&s)[8], uint32_t (&w)[16], uint32_t s0v, uint32_t h0_add) {
+    static_assert(R0 <= V && V >= 1 && V <= 15, "varying word");
+    static_for<R0, 63>([&](auto I) {
+        constexpr int t = decltype(I)::value;
+        if constexpr (t >= 16) {
+            uint32_t s0;
+            if constexpr (t - 15 == V)
+                s0 = s0v;
+            else
+                s0 = ssig0(w[(t - 15) & 15]);
+            w[t & 15] = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + s0 + w[t & 15];
+        }
+        sha_round<t>(s, w[t & 15]);
+    });
+    w[15] = ssig1(w[13]) + w[8] + ssig0(w[0]) + w[15];  // W[63]
+    const uint32_t a = s[1], b = s[2], c = s[3], e = s[5], f = s[6], g = s[7], h = s[0];  // roles at round 63
+    const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + (kK256[63] + h0_add) + w[15];
+    return t1 + bsig0(a) + maj(a, b, c);
+}
+
 // Full compression: st = st + F(st, block).
 BM_DEV void sha_compress(uint32_t (&st)[8], uint32_t (&w)[16]) {
     uint32_t s[8];
@@ -236,6 +273,9 @@ BM_DEV uint64_t readfirstlane_u64(uint64_t v) {
 // every 1-block inner loop spill-free; the layouts that carry a second
 // compression or a per-task block re-compression in registers get a larger
 // register budget (tools/check_inner.py verifies no spill lands in a loop).
+#ifndef BM_FOLD  // sha_rounds_h0's shortcuts in the inner loop (0 = plain rounds, for A/B)
+#define BM_FOLD 1
+#endif
 #ifndef BM_WAVES_PAD
 #define BM_WAVES_PAD 5
 #endif
@@ -260,6 +300,9 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
     // stepped by an outer loop in word LW-1 (round LW-1 redone per step), so
     // tasks stay 100 nonces long instead of 10.
     constexpr bool TWOW = (P % 4 == 0) && (LW >= 1);
+    // sha_rounds_h0's shortcuts (sigma0 split of word LW, H0 folded into
+    // round 63); the padding-block layouts keep the plain rounds.
+    constexpr bool kFold = BM_FOLD && !PADB && LW >= 1;
 
     // Inner-loop digit steps: digit i (< ms) of the inner counter sits at
     // bit 8*(3 - P%4 + i) of word LW.
@@ -338,6 +381,7 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
                     sha_rounds<LW - 1, LW>(s0, wo);
                 }
                 const uint32_t wl = wo[LW];
+                const uint32_t s0wl = ssig0(wl);  // sigma0 of word LW's task part (kFold)
 
                 // ---- inner loop over the uniform low digit(s) of word LW ----
                 uint32_t J = 0, c0 = 0, c1 = 0, c2 = 0;
@@ -349,10 +393,13 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
                     uint32_t x[8];
 #pragma unroll
                     for (int q = 0; q < 8; ++q) x[q] = s0[q];
-                    sha_rounds<LW, 64>(x, w);
 
                     uint32_t h0, h1;
-                    if constexpr (PADB) {
+                    if constexpr (kFold) {
+                        h0 = sha_rounds_h0<LW, LW>(x, w, s0wl ^ ssig0_uniform(J), st[0]);
+                        h1 = st[1] + x[1];
+                    } else if constexpr (PADB) {
+                        sha_rounds<LW, 64>(x, w);
                         uint32_t y[8];
 #pragma unroll
                         for (int q = 0; q < 8; ++q) y[q] = st[q] + x[q];
@@ -366,6 +413,7 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
                         h0 = y[0] + z[0];
                         h1 = y[1] + z[1];
                     } else {
+                        sha_rounds<LW, 64>(x, w);
                         h0 = st[0] + x[0];
                         h1 = st[1] + x[1];
                     }
