@@ -301,8 +301,11 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
     // tasks stay 100 nonces long instead of 10.
     constexpr bool TWOW = (P % 4 == 0) && (LW >= 1);
     // sha_rounds_h0's shortcuts (sigma0 split of word LW, H0 folded into
-    // round 63); the padding-block layouts keep the plain rounds.
-    constexpr bool kFold = BM_FOLD && !PADB && LW >= 1;
+    // round 63); the padding-block layouts keep the plain rounds, and so do
+    // the four whose inner loop would otherwise touch scratch
+    // (tools/check_inner.py).
+    constexpr bool kFold = BM_FOLD && !PADB && LW >= 1 && !(NBV == 1 && (P == 53 || P == 54)) &&
+                           !(NBV == 2 && P >= 17);
 
     // Inner-loop digit steps: digit i (< ms) of the inner counter sits at
     // bit 8*(3 - P%4 + i) of word LW.
