@@ -104,10 +104,74 @@ def cpu_baseline(target_s=10.0):
     t = time.perf_counter()
     oracle.search(MSG, hi - n + 1, hi, threads=threads, openssl=True)
     dt = time.perf_counter() - t
-    return {"value": n / dt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port",
-            "sample": f"msg 'bradfitz', last {n} nonces of [0, 2^32-1] (10-digit, 1 SHA-256 block each), "
-                      f"{threads} threads, snprintf-style format + OpenSSL SHA256 + strict '<' per nonce, "
-                      f"{dt:.1f} s"}
+    out = {"value": n / dt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port",
+           "sample": f"msg 'bradfitz', last {n} nonces of [0, 2^32-1] (10-digit, 1 SHA-256 block each), "
+                     f"{threads} threads, snprintf-style format + OpenSSL SHA256 + strict '<' per nonce, "
+                     f"{dt:.1f} s"}
+    want = oracle.search(MSG, hi - n + 1, hi, threads=threads, openssl=True)
+    try:
+        out["system"] = cpu_system_baseline(path, threads, hi - n + 1, hi, want)
+    except Exception as e:  # the system leg is informational; the figure above stands alone
+        out["system"] = {"error": repr(e)}
+    return out
+
+
+# One CPU miner process of the reference's architecture (miner.go:20-74: Join,
+# then Request -> sequential strict-'<' scan -> Result), its scan being the
+# oracle's single-threaded loop.  Test infrastructure: bench's cpu_baseline leg.
+_CPU_MINER = r"""
+import sys
+root, hostport, lib = sys.argv[1:4]
+sys.path[:0] = [root, root + "/tests"]
+from conftest import Oracle
+from distributed_bitcoin_minter_amd import lsp, miner
+from distributed_bitcoin_minter_amd.bitcoin import _as_bytes
+o = Oracle(lib)
+class Scan:
+    def search(self, data, lo, hi):
+        return o.search(_as_bytes(data), lo, hi, threads=1, openssl=True)
+miner.run(hostport, lsp.Params(EpochLimit=50, EpochMillis=100, WindowSize=1), searcher=Scan())
+"""
+
+
+def cpu_system_baseline(lib, n_miners, lo, hi, want, chunk_bits=24):
+    """SURVEY.md §8d CPU baseline as a system: one BitcoinServer + n_miners
+    single-threaded CPU miner processes + one client asking for [lo, hi] of
+    'bradfitz', all on this host (the reference's deployment: N Go miners
+    against one server).  GH/s = nonces / wall time from the request to the
+    answer; the answer must equal the oracle's scan of the same window."""
+    import subprocess
+    import threading
+    from distributed_bitcoin_minter_amd import client, lsp
+    from distributed_bitcoin_minter_amd.server import BitcoinServer
+
+    p = lsp.Params(EpochLimit=50, EpochMillis=100, WindowSize=1)
+    srv = lsp.NewServer(0, p)
+    bs = BitcoinServer(srv, chunk=1 << chunk_bits)
+    threading.Thread(target=bs.serve, daemon=True).start()
+    hostport = f"127.0.0.1:{srv.port}"
+    procs = [subprocess.Popen([sys.executable, "-c", _CPU_MINER, ROOT, hostport, lib],
+                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL) for _ in range(n_miners)]
+    try:
+        deadline = time.time() + 60
+        while bs.stats["joins"] < n_miners:
+            if time.time() > deadline or any(q.poll() is not None for q in procs):
+                raise RuntimeError(f"only {bs.stats['joins']} of {n_miners} CPU miners joined")
+            time.sleep(0.05)
+        t = time.perf_counter()
+        got = client.request(hostport, MSG.decode(), hi, p, lower=lo)
+        dt = time.perf_counter() - t
+    finally:
+        bs.close()
+        for q in procs:
+            q.kill()
+        for q in procs:
+            q.wait()
+    n = hi - lo + 1
+    return {"value": n / dt / 1e9, "unit": "GH/s", "cores": n_miners, "miners": n_miners,
+            "chunk": 1 << chunk_bits, "seconds": round(dt, 2), "result_ok": got == want,
+            "sample": f"one LSP server + {n_miners} single-threaded CPU miner processes + 1 client on "
+                      f"localhost, msg 'bradfitz', nonces [{lo}, {hi}], 2^{chunk_bits}-nonce chunks"}
 
 
 def main():
