@@ -18,7 +18,10 @@ Also reported:
                 on the library's stream, vs 78.64 T lane-ops/s per GPU.
   cpu_baseline  the CPU oracle's loop shape (format + SHA-256 + strict '<',
                 OpenSSL block code) on this host's cores over a bounded
-                sample of the same workload (rank 0, N = 1 only).
+                sample of the same workload (rank 0, N = 1 only); and, under
+                "system", the reference's deployment on the same cores: one
+                LSP server + N single-threaded CPU miner processes + a client
+                over the same window, its answer checked against the oracle.
 """
 import argparse
 import json
@@ -102,13 +105,12 @@ def cpu_baseline(target_s=10.0):
     rate = n / (time.perf_counter() - t)
     n = int(min(PER_GPU, max(n, rate * target_s)))
     t = time.perf_counter()
-    oracle.search(MSG, hi - n + 1, hi, threads=threads, openssl=True)
+    want = oracle.search(MSG, hi - n + 1, hi, threads=threads, openssl=True)
     dt = time.perf_counter() - t
     out = {"value": n / dt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port",
            "sample": f"msg 'bradfitz', last {n} nonces of [0, 2^32-1] (10-digit, 1 SHA-256 block each), "
                      f"{threads} threads, snprintf-style format + OpenSSL SHA256 + strict '<' per nonce, "
                      f"{dt:.1f} s"}
-    want = oracle.search(MSG, hi - n + 1, hi, threads=threads, openssl=True)
     try:
         out["system"] = cpu_system_baseline(path, threads, hi - n + 1, hi, want)
     except Exception as e:  # the system leg is informational; the figure above stands alone
