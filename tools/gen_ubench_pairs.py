@@ -37,6 +37,63 @@ CASES = [
     ("sub x8", ["v_sub_u32 {a%d}, {a%d}, {b}" % (i, i) for i in range(8)]),
     ("mov x8", ["v_mov_b32 {a%d}, {b}" % i for i in range(8)]),
     ("add_same_src x8", ["v_add_u32 {a%d}, {b}, {c}" % i for i in range(8)]),
+    # SGPR operands on ops that are slow anyway (the search loop's K constants sit in SGPRs)
+    ("add3_sgpr x8", ["v_add3_u32 {a%d}, {a%d}, {b}, {s}" % (i, i) for i in range(8)]),
+    ("bitop3_sgpr x8", ["v_bitop3_b32 {a%d}, {a%d}, {b}, {s} bitop3:0x96" % (i, i) for i in range(8)]),
+    ("alignbit_sgpr x8", ["v_alignbit_b32 {a%d}, {s}, {s}, 7" % i for i in range(8)]),
+    ("add3,xor,xor", sum([["v_add3_u32 {a%d}, {a%d}, {b}, {c}" % (i, i),
+                           "v_xor_b32 {a%d}, {a%d}, {b}" % ((i + 4) % 8, (i + 4) % 8),
+                           "v_xor_b32 {a%d}, {a%d}, {c}" % ((i + 5) % 8, (i + 5) % 8)] for i in range(0, 8, 2)], [])),
+    ("add3_sgpr,xor,xor", sum([["v_add3_u32 {a%d}, {a%d}, {b}, {s}" % (i, i),
+                                "v_xor_b32 {a%d}, {a%d}, {b}" % ((i + 4) % 8, (i + 4) % 8),
+                                "v_xor_b32 {a%d}, {a%d}, {c}" % ((i + 5) % 8, (i + 5) % 8)] for i in range(0, 8, 2)], [])),
+    ("add3,alignbit", sum([["v_add3_u32 {a%d}, {a%d}, {b}, {c}" % (i, i),
+                            "v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i + 1, i + 1, i + 1)] for i in range(0, 8, 2)], [])),
+    ("add3_sgpr,alignbit", sum([["v_add3_u32 {a%d}, {a%d}, {b}, {s}" % (i, i),
+                                 "v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i + 1, i + 1, i + 1)] for i in range(0, 8, 2)], [])),
+    # wave priority around slow / fast runs (s_setprio): does it let fast ops co-issue?
+    ("prio S0 F2: a,x,x", sum([["s_setprio 0", "v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i, i, i), "s_setprio 2",
+                                "v_xor_b32 {a%d}, {a%d}, {b}" % ((i + 4) % 8, (i + 4) % 8),
+                                "v_xor_b32 {a%d}, {a%d}, {c}" % ((i + 5) % 8, (i + 5) % 8)] for i in range(0, 8, 2)], [])),
+    ("prio S2 F0: a,x,x", sum([["s_setprio 2", "v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i, i, i), "s_setprio 0",
+                                "v_xor_b32 {a%d}, {a%d}, {b}" % ((i + 4) % 8, (i + 4) % 8),
+                                "v_xor_b32 {a%d}, {a%d}, {c}" % ((i + 5) % 8, (i + 5) % 8)] for i in range(0, 8, 2)], [])),
+    ("runs 4S 8F", ["v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i, i, i) for i in range(4)] +
+                   ["v_xor_b32 {a%d}, {a%d}, {b}" % (4 + i % 4, 4 + i % 4) for i in range(8)]),
+    ("prio runs 4S 8F", ["s_setprio 0"] + ["v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i, i, i) for i in range(4)] +
+                        ["s_setprio 2"] + ["v_xor_b32 {a%d}, {a%d}, {b}" % (4 + i % 4, 4 + i % 4) for i in range(8)]),
+    # one SHA-256 round + schedule word as grouped runs: 10 S (rotates), 9 F (xor3/shr/add/Ch/Maj),
+    # 4 S (add3), 1 F (e = d + T1); with and without priority toggles
+    ("sha grp S10F9S4F1", ["v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i % 8, i % 8, i % 8) for i in range(10)] +
+                          ["v_bitop3_b32 {a%d}, {a%d}, {b}, {c} bitop3:0x96" % (i % 8, i % 8) for i in range(9)] +
+                          ["v_add3_u32 {a%d}, {a%d}, {b}, {c}" % (i % 8, i % 8) for i in range(4)] +
+                          ["v_add_u32 {a0}, {a0}, {b}"]),
+    ("sha grp prio", ["s_setprio 2"] + ["v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i % 8, i % 8, i % 8) for i in range(10)] +
+                     ["s_setprio 0"] + ["v_bitop3_b32 {a%d}, {a%d}, {b}, {c} bitop3:0x96" % (i % 8, i % 8) for i in range(9)] +
+                     ["s_setprio 2"] + ["v_add3_u32 {a%d}, {a%d}, {b}, {c}" % (i % 8, i % 8) for i in range(4)] +
+                     ["s_setprio 0", "v_add_u32 {a0}, {a0}, {b}"]),
+    ("sha grp prio3", ["s_setprio 3"] + ["v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i % 8, i % 8, i % 8) for i in range(10)] +
+                      ["s_setprio 0"] + ["v_bitop3_b32 {a%d}, {a%d}, {b}, {c} bitop3:0x96" % (i % 8, i % 8) for i in range(9)] +
+                      ["s_setprio 3"] + ["v_add3_u32 {a%d}, {a%d}, {b}, {c}" % (i % 8, i % 8) for i in range(4)] +
+                      ["s_setprio 0", "v_add_u32 {a0}, {a0}, {b}"]),
+    ("prio runs 4S2 8F0", ["s_setprio 2"] + ["v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i, i, i) for i in range(4)] +
+                          ["s_setprio 0"] + ["v_xor_b32 {a%d}, {a%d}, {b}" % (4 + i % 4, 4 + i % 4) for i in range(8)]),
+    # the loop's actual interleaving (S,S,S,F,F,S,S,S,S,F,...) as compiled
+    ("sha fine", ["v_alignbit_b32 {a0}, {a0}, {a0}, 25", "v_alignbit_b32 {a1}, {a1}, {a1}, 11",
+                  "v_alignbit_b32 {a2}, {a2}, {a2}, 6", "v_bitop3_b32 {a3}, {a3}, {b}, {c} bitop3:0x96",
+                  "v_bitop3_b32 {a4}, {a4}, {b}, {c} bitop3:0xca", "v_add3_u32 {a5}, {a5}, {b}, {c}",
+                  "v_add3_u32 {a6}, {a6}, {b}, {c}", "v_alignbit_b32 {a7}, {a7}, {a7}, 22",
+                  "v_alignbit_b32 {a0}, {a0}, {a0}, 13", "v_alignbit_b32 {a1}, {a1}, {a1}, 2",
+                  "v_bitop3_b32 {a2}, {a2}, {b}, {c} bitop3:0x96", "v_bitop3_b32 {a3}, {a3}, {b}, {c} bitop3:0xe8",
+                  "v_add_u32 {a4}, {a4}, {b}", "v_add3_u32 {a5}, {a5}, {b}, {c}",
+                  "v_lshrrev_b32 {a6}, 3, {a6}", "v_alignbit_b32 {a7}, {a7}, {a7}, 18",
+                  "v_alignbit_b32 {a0}, {a0}, {a0}, 7", "v_bitop3_b32 {a1}, {a1}, {b}, {c} bitop3:0x96",
+                  "v_alignbit_b32 {a2}, {a2}, {a2}, 17", "v_alignbit_b32 {a3}, {a3}, {a3}, 19",
+                  "v_lshrrev_b32 {a4}, 10, {a4}", "v_bitop3_b32 {a5}, {a5}, {b}, {c} bitop3:0x96",
+                  "v_add_u32 {a6}, {a6}, {b}", "v_add3_u32 {a7}, {a7}, {b}, {c}"]),
+    ("nop-only SALU a,x,x",sum([["s_nop 0", "v_alignbit_b32 {a%d}, {a%d}, {a%d}, 7" % (i, i, i), "s_nop 0",
+                                  "v_xor_b32 {a%d}, {a%d}, {b}" % ((i + 4) % 8, (i + 4) % 8),
+                                  "v_xor_b32 {a%d}, {a%d}, {c}" % ((i + 5) % 8, (i + 5) % 8)] for i in range(0, 8, 2)], [])),
 ]
 
 
@@ -70,7 +127,7 @@ def emit():
     out.append('typedef void (*kfn)(unsigned*, unsigned long long*, unsigned);')
     out.append('static kfn ks[] = {' + ", ".join(f"k{i}" for i in range(len(CASES))) + '};')
     out.append('static const char* names[] = {' + ", ".join('"%s"' % n for n in names) + '};')
-    out.append('static const int ninstr[] = {' + ", ".join(str(len(l)) for _, l in CASES) + '};')
+    out.append('static const int ninstr[] = {' + ", ".join(str(sum(1 for x in l if x.startswith("v_"))) for _, l in CASES) + '};')
     out.append('''
 int main(int argc, char** argv) {
   int bpc = argc > 1 ? atoi(argv[1]) : 8;
