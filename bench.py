@@ -55,11 +55,13 @@ def compressions_per_nonce(msg_len, digits):
     return -(-(msg_len + digits + 10) // 64) - (msg_len + 1) // 64
 
 
-def instruction_mix_ceiling(p, nbv=1, clock_ghz=2.37):
-    """gfx950 issue-cost ceiling of the kernel's inner loop:
-    slow VALU (v_alignbit, v_add3, SGPR operands, ...) 4 SIMD-cycles, fast
-    2.24, from tools/isa_mix.py's static count of the compiled loop and the
-    clock measured under this kernel (GRBM_GUI_ACTIVE, profiles/r01)."""
+def issue_bound(p, nbv=1, clock_ghz=2.37):
+    """gfx950 VALU issue bound of the kernel's inner loop: each
+    slow op (v_alignbit, v_add3, SGPR operand, ...) takes an issue slot of its
+    own, fast ops of two waves share one, so a SIMD needs max(slow, (slow +
+    fast) / 2) slots of 4 cycles per 64 nonces; static counts from
+    tools/isa_mix.py on the built assembly, clock as measured under this
+    kernel (GRBM_GUI_ACTIVE, profiles/r01)."""
     path = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc", "isa_mix.json")
     try:
         lay = json.load(open(path))["layouts"][f"{p}:{nbv}"]
@@ -68,7 +70,7 @@ def instruction_mix_ceiling(p, nbv=1, clock_ghz=2.37):
     cyc = lay["simd_cycles_per_64_nonces"]
     ghs = 256 * 4 * clock_ghz * 1e9 * 64 / cyc / 1e9
     return {"valu_per_nonce": lay["valu"], "slow": lay["valu_slow"], "fast": lay["valu_fast"],
-            "clock_ghz": clock_ghz, "GHs_per_gpu": round(ghs, 2)}
+            "issue_slots_per_nonce": lay["issue_slots"], "clock_ghz": clock_ghz, "GHs_per_gpu": round(ghs, 2)}
 
 
 def pmc_traffic(p, nbv=1):
@@ -246,10 +248,12 @@ def main():
     dom_ms = sum(d[1] for d in doms) / len(doms)
     C = compressions_per_nonce(len(MSG), dom_digits)
     achieved = dom_nonces * C * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
-    mix = instruction_mix_ceiling(dom_p)
+    mix = issue_bound(dom_p)
     traffic, traffic_src, pmc = pmc_traffic(dom_p)
     # measured VALU per nonce (SQ_INSTS_VALU counts wave-instructions: x64 lanes)
     valu_pmc = pmc["SQ_INSTS_VALU"] * 64 / dom_nonces if "SQ_INSTS_VALU" in pmc else None
+    # fraction of VALU instructions issued as the second of a same-cycle pair (PMC)
+    valu2 = pmc["SQ_ACTIVE_INST_VALU2"] / pmc["SQ_INSTS_VALU"] if "SQ_ACTIVE_INST_VALU2" in pmc else None
     check = None
     if world == 1:
         check = list(res)  # C2 golden: (5256245051, 1626825724)
@@ -277,11 +281,12 @@ def main():
                      "traffic_note": "the per-launch dequeue counter's returning atomics (64-B memory-side "
                                      "requests); the search reads no input from HBM (DESIGN.md §5)",
                      "valu_per_nonce_pmc": valu_pmc and round(valu_pmc, 1),
+                     "valu_dual_issued_frac_pmc": valu2 and round(valu2, 4),
                      "kernel": f"search_kernel<P={dom_p},NBV=1> ({dom_digits}-digit nonces)",
                      "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom_nonces,
                      "ops_per_nonce": C * OPS_PER_COMPRESSION, "grid": dom_grid,
                      "tasks_per_thread": dom_tpt, "inner_digits": dom_inner,
-                     "mix_ceiling": mix and dict(mix, frac=round(dom_nonces / (dom_ms * 1e-3) / 1e9
+                     "issue_bound": mix and dict(mix, frac=round(dom_nonces / (dom_ms * 1e-3) / 1e9
                                                                   / mix["GHs_per_gpu"], 4))},
         "result": check,
     }

@@ -3,6 +3,7 @@
 search kernels' gfx950 assembly.
 
     bm_prio.py in.s out.s [--slow-prio 2] [--fast-prio 0] [--kernels search_kernel]
+                          [--min-fast-run 1] [--fold-sgpr 1]
 
 Why (tools/gen_ubench_pairs.py, profiles/r01/ubench_pairs4.log):
 on gfx950 two waves of a SIMD can issue VALU in the same cycle when the ops
@@ -16,8 +17,16 @@ for its fast runs (s_setprio 0) lets the slow op go first and the other
 waves' fast ops fill the second slot: a SHA-round-shaped microbenchmark goes
 from 1.84 to 2.47 wave-instructions per CU-cycle.
 
-The pass is purely an insertion of SOPP s_setprio instructions: it changes no
-VALU instruction, register or dependency, so results are unaffected (the GPU
+Before that, fold_sgpr_constants turns slow ops into fast ones where an SGPR
+operand provably holds a constant (its only definition in the kernel, or the
+last one in the block, is s_mov_b32 sN, imm): the SGPR becomes the literal,
+and v_add3_u32 x, y, K (slow) becomes two v_add_u32 (fast).  Fast ops cost
+little once they pair, so trading one slow op for two fast ones shortens the
+loop (C2 +1.8%, C3 +2.4%, profiles/r01/ab_fold_sgpr.log).
+
+The pass inserts SOPP s_setprio instructions and makes those two
+value-preserving rewrites; it changes no dependency, so results are
+unaffected (tests/test_prio_pass.py interprets a sample both ways; the GPU
 parity suite runs on the built library).  A toggle goes before the first
 VALU of every run whose class differs from the current priority; the state is
 reset at every label (any block may be entered from elsewhere).
@@ -46,28 +55,130 @@ def classify(mnemonic, operands):
             return "S"
     return "F"
 
+SREG_RE = re.compile(r"^s(\d+)$")
+SRANGE_RE = re.compile(r"^s\[(\d+):(\d+)\]$")
+VREG_RE = re.compile(r"^v\d+$")
+IMM_RE = re.compile(r"^(0x[0-9a-fA-F]+|-?\d+)$")
 
-def run(lines, kernels, slow, fast):
-    out, in_kernel, cur = [], False, None
-    n_toggle = n_valu = 0
-    for line in lines:
+
+def _operands(rest):
+    return [o.strip() for o in rest.split(" bitop3:")[0].split(",") if o.strip()]
+
+
+def _sdefs(line):
+    """SGPR numbers an instruction writes (its first operand), conservatively."""
+    m = re.match(r"^\s+([sv]_[a-z0-9_]+)\s*(.*)$", line)
+    if not m or m.group(1).startswith(("s_cmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "s_setprio",
+                                        "s_endpgm", "s_barrier", "s_sleep")):
+        return []
+    ops = _operands(m.group(2))
+    if not ops:
+        return []
+    d = ops[0]
+    if SREG_RE.match(d):
+        return [int(SREG_RE.match(d).group(1))]
+    r = SRANGE_RE.match(d)
+    if r:
+        return list(range(int(r.group(1)), int(r.group(2)) + 1))
+    return []
+
+
+def fold_sgpr_constants(lines, kernels):
+    """Replace SGPR operands holding a known constant by the literal, so the
+    VALU op stays in the fast class, and split v_add3_u32 with such an
+    operand into two v_add_u32 (two fast ops for one slow one).  A constant is
+    known when the SGPR's only definition in the kernel is s_mov_b32 sN, imm,
+    or, inside a block, since the last s_mov_b32 sN, imm."""
+    out, i, n_fold, n_split = [], 0, 0, 0
+    while i < len(lines):
+        m_fn = re.match(r"^(_Z\S+):", lines[i])
+        if not (m_fn and any(k in m_fn.group(1) for k in kernels)):
+            out.append(lines[i])
+            i += 1
+            continue
+        j = i
+        while j < len(lines) and not lines[j].startswith(".Lfunc_end"):
+            j += 1
+        body = lines[i:j]
+        defs, single = {}, {}
+        for ln in body:
+            for r in _sdefs(ln):
+                defs[r] = defs.get(r, 0) + 1
+        for ln in body:
+            m = re.match(r"^\s+s_mov_b32 s(\d+), (\S+)\s*$", ln)
+            if m and defs.get(int(m.group(1))) == 1 and IMM_RE.match(m.group(2)):
+                single[int(m.group(1))] = m.group(2)
+        local = {}
+        for ln in body:
+            if re.match(r"^[.%$\w]+:", ln) or ln.startswith("; %bb"):
+                local = {}
+            m = re.match(r"^\s+(v_add3_u32|v_add_u32_e32|v_xor_b32_e32)\s+(.*)$", ln)
+            if m:
+                ops = _operands(m.group(2))
+                known = lambda o: (local.get(int(SREG_RE.match(o).group(1))) or single.get(int(SREG_RE.match(o).group(1)))) \
+                    if SREG_RE.match(o) else None
+                if m.group(1) == "v_add3_u32" and len(ops) == 4:
+                    ks = [k for k in range(1, 4) if known(ops[k])]
+                    vs = [k for k in range(1, 4) if VREG_RE.match(ops[k])]
+                    if len(ks) == 1 and len(vs) == 2:
+                        lit = known(ops[ks[0]])
+                        x, y = ops[vs[0]], ops[vs[1]]
+                        out.append(f"\tv_add_u32_e32 {ops[0]}, {x}, {y}\n")
+                        out.append(f"\tv_add_u32_e32 {ops[0]}, {lit}, {ops[0]}\n")
+                        n_split += 1
+                        continue
+                elif len(ops) == 3 and known(ops[1]) and VREG_RE.match(ops[2]):
+                    out.append(f"\t{m.group(1)} {ops[0]}, {known(ops[1])}, {ops[2]}\n")
+                    n_fold += 1
+                    continue
+            for r in _sdefs(ln):
+                local.pop(r, None)
+            m = re.match(r"^\s+s_mov_b32 s(\d+), (\S+)\s*$", ln)
+            if m and IMM_RE.match(m.group(2)):
+                local[int(m.group(1))] = m.group(2)
+            out.append(ln)
+        i = j
+    return out, n_fold, n_split
+
+
+def run(lines, kernels, slow, fast, min_fast_run=1):
+    """Insert the toggles.  A fast run shorter than min_fast_run VALU (counted
+    up to the next label) keeps the slow priority."""
+    cls = [None] * len(lines)  # VALU class per line (None: not a VALU / not in a search kernel)
+    in_kernel = False
+    for i, line in enumerate(lines):
         m_fn = re.match(r"^(_Z\S+):", line)
         if m_fn:
             in_kernel = any(k in m_fn.group(1) for k in kernels)
-            cur = None
         elif line.startswith(".Lfunc_end"):
             in_kernel = False
         if in_kernel:
             if re.match(r"^[.%$\w]+:", line) or line.startswith("; %bb"):
-                cur = None  # block entry: priority unknown
+                cls[i] = "L"  # label: block boundary
+                continue
             m = INSN_RE.match(line)
             if m and not m.group(1).startswith(("v_readlane", "v_readfirstlane", "v_writelane", "v_nop")):
-                n_valu += 1
-                c = classify(m.group(1), m.group(2))
-                if c != cur:
-                    out.append(f"\ts_setprio {slow if c == 'S' else fast}\n")
-                    n_toggle += 1
-                    cur = c
+                cls[i] = classify(m.group(1), m.group(2))
+    out, cur = [], None
+    n_toggle = n_valu = 0
+    for i, line in enumerate(lines):
+        c = cls[i]
+        if c == "L":
+            cur = None
+        elif c in ("S", "F"):
+            n_valu += 1
+            want = c
+            if c == "F" and min_fast_run > 1:
+                run_len, j = 0, i
+                while j < len(lines) and cls[j] != "L" and cls[j] != "S" and run_len < min_fast_run:
+                    run_len += cls[j] == "F"
+                    j += 1
+                if run_len < min_fast_run and cur == "S":
+                    want = "S"
+            if want != cur:
+                out.append(f"\ts_setprio {slow if want == 'S' else fast}\n")
+                n_toggle += 1
+                cur = want
         out.append(line)
     return out, n_toggle, n_valu
 
@@ -79,9 +190,14 @@ def main():
     ap.add_argument("--slow-prio", type=int, default=2)
     ap.add_argument("--fast-prio", type=int, default=0)
     ap.add_argument("--kernels", default="search_kernel")
+    ap.add_argument("--min-fast-run", type=int, default=1)
+    ap.add_argument("--fold-sgpr", type=int, default=1, help="1: literal-fold known SGPR constants, split add3")
     a = ap.parse_args()
     lines = open(a.src).readlines()
-    out, n_toggle, n_valu = run(lines, a.kernels.split(","), a.slow_prio, a.fast_prio)
+    if a.fold_sgpr:
+        lines, n_fold, n_split = fold_sgpr_constants(lines, a.kernels.split(","))
+        print(f"bm_prio: {a.src}: {n_fold} SGPR constants folded, {n_split} v_add3 split", file=sys.stderr)
+    out, n_toggle, n_valu = run(lines, a.kernels.split(","), a.slow_prio, a.fast_prio, a.min_fast_run)
     open(a.dst, "w").writelines(out)
     print(f"bm_prio: {a.src}: {n_toggle} s_setprio over {n_valu} VALU", file=sys.stderr)
 

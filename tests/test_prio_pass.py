@@ -1,0 +1,132 @@
+"""csrc/bm_prio.py, the build step that adds wave-priority toggles to the
+search kernels' assembly and folds known SGPR constants (CPU only).
+
+The pass must not change what the kernel computes: it only inserts
+s_setprio, replaces an SGPR operand by the literal the SGPR provably holds,
+and splits v_add3_u32 x, y, K into two v_add_u32.  A small interpreter for
+the ops involved checks that on random register values."""
+import os
+import random
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc"))
+
+import bm_prio  # noqa: E402
+
+M32 = 0xFFFFFFFF
+
+KERNEL = """\
+_ZN2bm13search_kernelILi18ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
+\ts_mov_b32 s16, 0x923f82a4
+.LBB5_1:
+\tv_add_u32_e32 v20, s55, v26
+\tv_alignbit_b32 v10, v7, v7, 25
+\tv_bitop3_b32 v10, v21, v11, v10 bitop3:0x96
+\ts_mov_b32 s10, 0x1e376c08
+\tv_add3_u32 v2, v2, v3, s10
+\tv_add3_u32 v3, s16, v9, v3
+\tv_add_u32_e32 v46, s16, v46
+\tv_lshrrev_b32_e32 v47, 10, v44
+\tv_add3_u32 v11, v3, v10, v2
+\ts_cbranch_scc1 .LBB5_1
+.Lfunc_end5:
+"""
+
+
+def run_block(lines, regs):
+    """Interpret the straight-line ops of the test kernel."""
+    r = dict(regs)
+
+    def val(o):
+        o = o.strip()
+        if o.startswith(("v", "s")) and o[1:].isdigit():
+            return r[o]
+        return int(o, 0) & M32
+
+    for ln in lines:
+        t = ln.strip()
+        if not t or t.endswith(":") or t.startswith(("s_setprio", "s_cbranch", ".", "_Z")):
+            continue
+        op, rest = t.split(None, 1)
+        ops = [o.strip() for o in rest.split(" bitop3:")[0].split(",")]
+        d = ops[0]
+        if op == "s_mov_b32":
+            r[d] = val(ops[1])
+        elif op == "v_add_u32_e32":
+            r[d] = (val(ops[1]) + val(ops[2])) & M32
+        elif op == "v_add3_u32":
+            r[d] = (val(ops[1]) + val(ops[2]) + val(ops[3])) & M32
+        elif op == "v_lshrrev_b32_e32":
+            r[d] = val(ops[2]) >> val(ops[1])
+        elif op == "v_alignbit_b32":
+            r[d] = (((val(ops[1]) << 32) | val(ops[2])) >> (val(ops[3]) & 31)) & M32
+        elif op == "v_bitop3_b32":
+            assert "bitop3:0x96" in t
+            r[d] = val(ops[1]) ^ val(ops[2]) ^ val(ops[3])
+        else:
+            raise AssertionError(op)
+    return r
+
+
+def test_classify():
+    assert bm_prio.classify("v_add_u32_e32", "v1, v2, v3") == "F"
+    assert bm_prio.classify("v_add_u32_e32", "v1, 0x1234, v3") == "F"
+    assert bm_prio.classify("v_add_u32_e32", "v1, s5, v3") == "S"        # SGPR operand
+    assert bm_prio.classify("v_bitop3_b32", "v1, v2, v3, v4 bitop3:0x96") == "F"
+    assert bm_prio.classify("v_bitop3_b32", "v1, v2, s3, v4 bitop3:0x96") == "S"
+    assert bm_prio.classify("v_alignbit_b32", "v1, v2, v2, 7") == "S"
+    assert bm_prio.classify("v_add3_u32", "v1, v2, v3, v4") == "S"
+    assert bm_prio.classify("v_lshlrev_b32_e32", "v1, 3, v2") == "S"
+    assert bm_prio.classify("v_lshrrev_b32_e32", "v1, 3, v2") == "F"
+    assert bm_prio.classify("v_xor_b32_sdwa", "v1, v2, v3") == "S"
+
+
+def test_toggles_at_run_starts_and_labels():
+    lines = KERNEL.splitlines(keepends=True)
+    out, n_toggle, n_valu = bm_prio.run(lines, ["search_kernel"], 2, 0)
+    body = [l.strip() for l in out]
+    assert n_valu == 8
+    # every VALU is preceded (within its run) by the toggle of its class
+    cur = None
+    for t in body:
+        if t.endswith(":"):
+            cur = None
+        elif t.startswith("s_setprio"):
+            cur = int(t.split()[1])
+        elif t.startswith("v_"):
+            cls = bm_prio.classify(t.split()[0], t.split(None, 1)[1])
+            assert cur == (2 if cls == "S" else 0), t
+    # a label resets the state: the first VALU after .LBB5_1 has its own toggle
+    i = body.index(".LBB5_1:")
+    assert body[i + 1].startswith("s_setprio")
+
+
+def test_fold_and_split_keep_results():
+    lines = KERNEL.splitlines(keepends=True)
+    out, n_fold, n_split = bm_prio.fold_sgpr_constants(lines, ["search_kernel"])
+    text = "".join(out)
+    assert n_split == 2 and n_fold == 1, (n_fold, n_split)
+    assert "v_add3_u32 v2, v2, v3, s10" not in text          # split with the block-local constant
+    assert "v_add_u32_e32 v46, 0x923f82a4, v46" in text       # single-definition constant folded
+    assert "v_add3_u32 v11, v3, v10, v2" in text              # all-VGPR add3 untouched
+    final, _, _ = bm_prio.run(out, ["search_kernel"], 2, 0)
+    rng = random.Random(7)
+    for _ in range(200):
+        regs = {f"v{i}": rng.getrandbits(32) for i in range(64)}
+        regs.update({f"s{i}": rng.getrandbits(32) for i in range(64)})
+        assert run_block(lines, regs) == run_block(final, regs)
+
+
+def test_multi_def_sgpr_not_folded_across_blocks():
+    src = """\
+_ZN2bm13search_kernelILi5ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
+\ts_mov_b32 s10, 7
+.LBB1_1:
+\tv_add_u32_e32 v1, s10, v1
+\ts_mov_b32 s10, 9
+\ts_cbranch_scc1 .LBB1_1
+.Lfunc_end1:
+"""
+    out, n_fold, n_split = bm_prio.fold_sgpr_constants(src.splitlines(keepends=True), ["search_kernel"])
+    assert n_fold == 0 and n_split == 0   # s10 has two definitions; at the loop head it is not known

@@ -26,6 +26,6 @@ fi
 if [ "${PMC:-1}" = "1" ]; then
   step pmc_fetch 90 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o f --output-format csv -- python3 tools/prof_one.py C2
   step pmc_write 90 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o w --output-format csv -- python3 tools/prof_one.py C2
-  step pmc_sq 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o s --output-format csv -- python3 tools/prof_one.py C2
+  step pmc_sq 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o s --output-format csv -- python3 tools/prof_one.py C2
 fi
 echo done

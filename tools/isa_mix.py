@@ -1,25 +1,27 @@
 #!/usr/bin/env python3
-"""Per-nonce VALU mix of the search kernel's inner loop for given layouts,
-classified with the gfx950 issue costs measured in profiles/r01/ubench_*.log
-(DESIGN.md §5).  Writes distributed_bitcoin_minter_amd/csrc/isa_mix.json,
-which bench.py reads to report the instruction-mix ceiling.
+"""Per-nonce VALU mix of the search kernel's inner loop for given layouts, read
+from the built assembly (after csrc/bm_prio.py) and classified as bm_prio.py
+does: fast ops (co-issue with another wave's fast op) and slow ops (issue
+alone).  Issue bound per 64 nonces = 4 SIMD-cycles x max(slow, (slow+fast)/2):
+every slow op takes an issue slot of its own, fast ops fill the second slot
+beside it.  Writes distributed_bitcoin_minter_amd/csrc/
+isa_mix.json, which bench.py reads to report the issue bound.
 
     python tools/isa_mix.py 18:1 12:1 ...      (P:NBV pairs; default 18:1 12:1)
 """
 import json
 import os
 import re
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc")
 sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, CSRC)
+import bm_prio  # noqa: E402
 import isa_loops  # noqa: E402
 
-FAST = re.compile(r"^v_(add_u32|sub_u32|subrev_u32|xor_b32|or_b32|and_b32|not_b32|lshrrev_b32|ashrrev_i32|"
-                  r"bitop3_b32|mov_b32|add_f32|fma_f32|mul_f32)(_e32|_e64)?$")
-CYC_SLOW, CYC_FAST = 4.0, 2.24
+CYC_SLOT = 4.0  # SIMD-cycles per issue slot (one slow op, or two fast ops of two waves)
 
 
 def inner_ops(sfile, kernel_sub):
@@ -46,29 +48,37 @@ def inner_ops(sfile, kernel_sub):
 def classify(ops):
     fast = slow = 0
     for op, text in ops:
-        if not op.startswith("v_"):
+        if not op.startswith("v_") or op.startswith(("v_readlane", "v_readfirstlane", "v_writelane")):
             continue
-        sgpr = re.search(r"\bs\[?\d", text.split(None, 1)[1] if " " in text else "")
-        if FAST.match(op) and not sgpr:
+        rest = text.split(None, 1)[1] if " " in text else ""
+        if bm_prio.classify(op, rest) == "F":
             fast += 1
         else:
             slow += 1
     return fast, slow
 
 
+def asm_file(p, nbv):
+    ranges = {1: ["0_7", "8_15", "16_23", "24_31", "32_39", "40_47", "48_55", "56_63"],
+              2: ["0_4", "5_9", "10_14", "15_18"]}[nbv]
+    for r in ranges:
+        lo, hi = map(int, r.split("_"))
+        if lo <= p <= hi:
+            return os.path.join(CSRC, "build", f"inst{nbv}_{r}-hip-amdgcn-amd-amdhsa-gfx950.s")
+    raise ValueError((p, nbv))
+
+
 def main():
     pairs = sys.argv[1:] or ["18:1", "12:1"]
-    out = {"cycles": {"slow": CYC_SLOW, "fast": CYC_FAST},
-           "source": "tools/isa_mix.py on hipcc -O3 gfx950 output", "layouts": {}}
+    out = {"cycles_per_slot": CYC_SLOT, "model": "slots per 64 nonces = max(slow, (slow + fast) / 2)",
+           "source": "tools/isa_mix.py on the built assembly (hipcc -O3 gfx950 + csrc/bm_prio.py)", "layouts": {}}
     for pr in pairs:
-        p, nbv = pr.split(":")
-        subprocess.check_call(["make", "-s", "-C", CSRC, "isa", f"P={p}", f"NBV={nbv}"],
-                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-        sfile = os.path.join(CSRC, "build", "bm_inst-hip-amdgcn-amd-amdhsa-gfx950.s")
-        ops = inner_ops(sfile, f"search_kernelILi{p}ELi{nbv}E")
+        p, nbv = map(int, pr.split(":"))
+        ops = inner_ops(asm_file(p, nbv), f"search_kernelILi{p}ELi{nbv}E")
         fast, slow = classify(ops)
+        slots = max(slow, (slow + fast) / 2)
         out["layouts"][f"{p}:{nbv}"] = {"valu_fast": fast, "valu_slow": slow, "valu": fast + slow,
-                                        "simd_cycles_per_64_nonces": slow * CYC_SLOW + fast * CYC_FAST}
+                                        "issue_slots": slots, "simd_cycles_per_64_nonces": slots * CYC_SLOT}
         print(pr, out["layouts"][f"{p}:{nbv}"])
     json.dump(out, open(os.path.join(CSRC, "isa_mix.json"), "w"), indent=1)
 
