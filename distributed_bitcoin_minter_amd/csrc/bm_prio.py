@@ -141,6 +141,41 @@ def fold_sgpr_constants(lines, kernels):
     return out, n_fold, n_split
 
 
+def split_add3(lines, kernels, every):
+    """Split every `every`-th all-VGPR v_add3_u32 d, a, b, c of the search
+    kernels into v_add_u32 d, x, y; v_add_u32 d, z, d.  The loop is slow-slot
+    bound (S > (S+F)/2): each split moves one op from the slow
+    class to two in the fast class, and the issue bound max(S, (S+F)/2) falls
+    until the two terms meet (about 1 in 8 of the C2 loop's add3).  The pair
+    whose first add overwrites d must read every source equal to d."""
+    out, n, seen, in_kernel = [], 0, 0, False
+    for ln in lines:
+        m_fn = re.match(r"^(_Z\S+):", ln)
+        if m_fn:
+            in_kernel = any(k in m_fn.group(1) for k in kernels)
+        elif ln.startswith(".Lfunc_end"):
+            in_kernel = False
+        m = re.match(r"^\s+v_add3_u32\s+(.*)$", ln) if in_kernel else None
+        if m:
+            ops = _operands(m.group(1))
+            if len(ops) == 4 and all(VREG_RE.match(o) for o in ops):
+                d, srcs = ops[0], ops[1:]
+                hits = [s for s in srcs if s == d]
+                rest = [s for s in srcs if s != d]
+                if len(hits) < 3:
+                    seen += 1
+                    if seen % every == 0:
+                        first = (hits + rest)[:2]   # every read of d happens in the first add
+                        last = (hits + rest)[2]
+                        if len(hits) <= 2 and last != d:
+                            out.append(f"\tv_add_u32_e32 {d}, {first[0]}, {first[1]}\n")
+                            out.append(f"\tv_add_u32_e32 {d}, {last}, {d}\n")
+                            n += 1
+                            continue
+        out.append(ln)
+    return out, n
+
+
 def run(lines, kernels, slow, fast, min_fast_run=1):
     """Insert the toggles.  A fast run shorter than min_fast_run VALU (counted
     up to the next label) keeps the slow priority."""
@@ -192,11 +227,16 @@ def main():
     ap.add_argument("--kernels", default="search_kernel")
     ap.add_argument("--min-fast-run", type=int, default=1)
     ap.add_argument("--fold-sgpr", type=int, default=1, help="1: literal-fold known SGPR constants, split add3")
+    ap.add_argument("--split-add3-every", type=int, default=0,
+                    help="K > 0: split every K-th all-VGPR v_add3_u32 into two v_add_u32")
     a = ap.parse_args()
     lines = open(a.src).readlines()
     if a.fold_sgpr:
         lines, n_fold, n_split = fold_sgpr_constants(lines, a.kernels.split(","))
         print(f"bm_prio: {a.src}: {n_fold} SGPR constants folded, {n_split} v_add3 split", file=sys.stderr)
+    if a.split_add3_every:
+        lines, n_split3 = split_add3(lines, a.kernels.split(","), a.split_add3_every)
+        print(f"bm_prio: {a.src}: {n_split3} all-VGPR v_add3 split", file=sys.stderr)
     out, n_toggle, n_valu = run(lines, a.kernels.split(","), a.slow_prio, a.fast_prio, a.min_fast_run)
     open(a.dst, "w").writelines(out)
     print(f"bm_prio: {a.src}: {n_toggle} s_setprio over {n_valu} VALU", file=sys.stderr)

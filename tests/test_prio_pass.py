@@ -130,3 +130,29 @@ _ZN2bm13search_kernelILi5ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
 """
     out, n_fold, n_split = bm_prio.fold_sgpr_constants(src.splitlines(keepends=True), ["search_kernel"])
     assert n_fold == 0 and n_split == 0   # s10 has two definitions; at the loop head it is not known
+
+
+def test_split_all_vgpr_add3_keeps_results_with_aliased_dest():
+    """--split-add3-every (measured, not on by default: profiles/r01/ab_split_add3.log)."""
+    src = """\
+_ZN2bm13search_kernelILi18ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
+.LBB5_1:
+\tv_add3_u32 v1, v2, v3, v4
+\tv_add3_u32 v2, v3, v4, v2
+\tv_add3_u32 v3, v3, v5, v3
+\tv_add3_u32 v4, v4, v4, v4
+\tv_add3_u32 v5, v1, s3, v2
+\ts_cbranch_scc1 .LBB5_1
+.Lfunc_end5:
+"""
+    lines = src.splitlines(keepends=True)
+    out, n = bm_prio.split_add3(lines, ["search_kernel"], 1)
+    assert n == 3                                  # d == every source, and SGPR operands, stay add3
+    assert "v_add3_u32 v4, v4, v4, v4" in "".join(out)
+    rng = random.Random(11)
+    for _ in range(200):
+        regs = {f"v{i}": rng.getrandbits(32) for i in range(8)}
+        regs.update({f"s{i}": rng.getrandbits(32) for i in range(8)})
+        assert run_block(lines, regs) == run_block(out, regs)
+    out2, n2 = bm_prio.split_add3(lines, ["search_kernel"], 2)
+    assert n2 == 1
