@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -26,6 +27,12 @@ static const void* g_search[2][64];
 constexpr int kMaxInnerDigits = 2;  // S <= 100 nonces per task: small dequeue chunks, short tail
 constexpr uint32_t kNoncesPerLaneChunk = 100;
 constexpr int kEventPairs = BM_MAX_LAUNCH_STATS;
+// Launch streams per device.  Every search launch is a persistent grid that
+// drains a work counter, so its last tasks leave CUs idle (about half a
+// 100-nonce task, ~0.5 ms).  With more than one stream the launches of one
+// call go out biggest first over the streams, and the next launch's
+// workgroups fill the CUs the previous one frees.
+constexpr int kMaxStreams = 4;
 
 struct DeviceCtx {
     int id = -1;
@@ -41,6 +48,8 @@ struct DeviceCtx {
     uint64_t* d_hash_io = nullptr;
     size_t hash_cap = 0;
     hipEvent_t ev[2 * kEventPairs] = {};
+    hipStream_t aux[kMaxStreams - 1] = {};  // extra launch streams (ctx->streams > 1)
+    hipEvent_t fork = nullptr, join[kMaxStreams - 1] = {};
     ncclComm_t comm = nullptr;
     std::vector<std::pair<const void*, int>> occ;  // kernel -> blocks per CU
 };
@@ -82,6 +91,7 @@ struct bm_ctx {
     int max_windows = bm::kDefaultMaxWindows;
     int combine = BM_COMBINE_AUTO;
     int task_digits = 0;  // 0: per launch (size_launch); 1 or 2: forced
+    int streams = 2;      // launch streams per device (1..kMaxStreams; BTCMINER_STREAMS; profiles/r01/ab_streams.log)
     bool nccl_ready = false;
     bm_stats_t stats;
 };
@@ -205,6 +215,9 @@ int init_device(DeviceCtx& d, int id, int ndev) {
     BM_HIP(hipMalloc(&d.d_gather, sizeof(Partial) * (size_t)ndev));
     BM_HIP(hipHostMalloc(&d.h_result, sizeof(Partial) * (size_t)ndev, hipHostMallocDefault));
     for (auto& e : d.ev) BM_HIP(hipEventCreate(&e));
+    for (auto& s : d.aux) BM_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    BM_HIP(hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
+    for (auto& e : d.join) BM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     int rc = ensure_counters(d, 256);
     if (rc != BM_OK) return rc;
     return ensure_partials(d, 4096);
@@ -214,6 +227,8 @@ void destroy_device(DeviceCtx& d) {
     if (d.id < 0) return;
     (void)hipSetDevice(d.id);
     if (d.stream) (void)hipStreamSynchronize(d.stream);
+    for (auto& s : d.aux)
+        if (s) (void)hipStreamSynchronize(s);
     if (d.comm) (void)ncclCommDestroy(d.comm);
     for (auto& e : d.ev)
         if (e) (void)hipEventDestroy(e);
@@ -223,6 +238,11 @@ void destroy_device(DeviceCtx& d) {
     if (d.d_gather) (void)hipFree(d.d_gather);
     if (d.d_hash_io) (void)hipFree(d.d_hash_io);
     if (d.h_result) (void)hipHostFree(d.h_result);
+    for (auto& e : d.join)
+        if (e) (void)hipEventDestroy(e);
+    if (d.fork) (void)hipEventDestroy(d.fork);
+    for (auto& s : d.aux)
+        if (s) (void)hipStreamDestroy(s);
     if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -281,15 +301,32 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         uint32_t nparts = 0, li = 0;
         if (!launches[di].empty())
             BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches[di].size() * sizeof(unsigned long long), d.stream));
-        for (Launch& L : launches[di]) {
+        // stream of each launch: biggest first, round-robin over the streams
+        const int ns = std::max(1, std::min<int>(ctx->streams, (int)launches[di].size()));
+        std::vector<uint32_t> order(launches[di].size());
+        for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
+        if (ns > 1) {
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+                return launches[di][a].stat.nonces > launches[di][b].stat.nonces;
+            });
+            BM_HIP(hipEventRecord(d.fork, d.stream));
+            for (int k = 0; k + 1 < ns; ++k) BM_HIP(hipStreamWaitEvent(d.aux[k], d.fork, 0));
+        }
+        for (uint32_t r = 0; r < order.size(); ++r) {
+            li = order[r];
+            Launch& L = launches[di][li];
+            hipStream_t s = (r % ns) == 0 ? d.stream : d.aux[r % ns - 1];
             const bool timed = ctx->timing && li < (uint32_t)kEventPairs;
-            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li], d.stream));
+            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li], s));
             unsigned long long* ctr = d.d_ctr + li;
             void* kargs[] = {&L.args, &d.d_part, &ctr};
-            BM_HIP(hipLaunchKernel(L.fn, dim3(L.grid), dim3(kBlock), kargs, 0, d.stream));
-            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li + 1], d.stream));
+            BM_HIP(hipLaunchKernel(L.fn, dim3(L.grid), dim3(kBlock), kargs, 0, s));
+            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li + 1], s));
             nparts += L.grid;
-            ++li;
+        }
+        for (int k = 0; k + 1 < ns; ++k) {
+            BM_HIP(hipEventRecord(d.join[k], d.aux[k]));
+            BM_HIP(hipStreamWaitEvent(d.stream, d.join[k], 0));
         }
         reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, d.d_result);
         BM_HIP(hipGetLastError());
@@ -435,6 +472,10 @@ int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out) {
     bm_ctx* ctx = new (std::nothrow) bm_ctx();
     if (!ctx) return BM_ENOMEM;
     std::memset(&ctx->stats, 0, sizeof ctx->stats);
+    if (const char* e = std::getenv("BTCMINER_STREAMS")) {
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= bm::kMaxStreams) ctx->streams = v;
+    }
     bm::DeviceGuard guard;
     ctx->devs.resize(n);
     for (int i = 0; i < n; ++i) {

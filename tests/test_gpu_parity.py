@@ -195,3 +195,19 @@ def test_c4_shape_single_process(gpu_ctx, oracle):
     assert min(gpu_ctx.search(msg, lo, mid), gpu_ctx.search(msg, mid + 1, hi)) == (h, n)
     a, b = max(lo, n - 20000), min(hi, n + 20000)
     assert oracle.search(msg, a, b, threads=8) == (h, n)
+
+
+@pytest.mark.parametrize("streams", [1, 2, 4])
+def test_launch_streams(oracle, monkeypatch, streams):
+    """Launches of one call spread over 1, 2 or 4 streams (BTCMINER_STREAMS,
+    read at context creation; default 2): the multi-launch ranges (every digit
+    length from 1, a 19/20-digit boundary, the C2 range) give the same answers,
+    and the small windows equal the oracle."""
+    from distributed_bitcoin_minter_amd import Context
+    monkeypatch.setenv("BTCMINER_STREAMS", str(streams))
+    c2 = next(c for c in load_golden("full_range.json")["cases"] if c["config"] == "C2")
+    with Context(devices=[0]) as c:
+        assert c.search(b"bradfitz", 0, 9999) == (1419516646206828, 9898)
+        for msg, lo, hi in ((b"bradfitz", 0, 3_000_000), (M120, 10**19 - 1_500_000, 10**19 + 1_500_000)):
+            assert c.search(msg, lo, hi) == oracle.search(msg, lo, hi, threads=8)
+        assert c.search(bytes.fromhex(c2["msg_hex"]), c2["lower"], c2["upper"]) == (c2["hash"], c2["nonce"])
