@@ -91,6 +91,7 @@ struct bm_ctx {
     int max_windows = bm::kDefaultMaxWindows;
     int combine = BM_COMBINE_AUTO;
     int task_digits = 0;  // 0: per launch (size_launch); 1 or 2: forced
+    uint64_t tail_nonces = 1ull << 24;  // split off the biggest launch's last nonces (BTCMINER_TAIL; 0: off; profiles/r01/ab_tail.log)
     int streams = 2;      // launch streams per device (1..kMaxStreams; BTCMINER_STREAMS; profiles/r01/ab_streams.log)
     bool nccl_ready = false;
     bm_stats_t stats;
@@ -278,6 +279,22 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         std::vector<bm_segment_t> segs;
         int rc = plan_segments(msg, len, pieces[di].lo, pieces[di].hi, segs, ctx->max_windows);
         if (rc != BM_OK) return rc;
+        // With streams to overlap on, the biggest segment's last tail_nonces
+        // become a launch of their own: it is small enough for 10-nonce tasks
+        // (size_launch), so the call ends on a short drain instead of half a
+        // 100-nonce task.
+        if (ctx->streams > 1 && ctx->tail_nonces > 0 && !segs.empty()) {
+            size_t big = 0;
+            for (size_t i = 1; i < segs.size(); ++i)
+                if (segs[i].vhi - segs[i].vlo > segs[big].vhi - segs[big].vlo) big = i;
+            bm_segment_t& b = segs[big];
+            if (b.vhi - b.vlo >= 8 * ctx->tail_nonces) {
+                bm_segment_t t = b;
+                t.vlo = b.vhi - ctx->tail_nonces + 1;
+                b.vhi = t.vlo - 1;
+                segs.push_back(t);
+            }
+        }
         uint32_t off = 0;
         for (const auto& s : segs) {
             Launch L;
@@ -476,6 +493,7 @@ int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out) {
         const int v = std::atoi(e);
         if (v >= 1 && v <= bm::kMaxStreams) ctx->streams = v;
     }
+    if (const char* e = std::getenv("BTCMINER_TAIL")) ctx->tail_nonces = std::strtoull(e, nullptr, 10);
     bm::DeviceGuard guard;
     ctx->devs.resize(n);
     for (int i = 0; i < n; ++i) {

@@ -211,3 +211,17 @@ def test_launch_streams(oracle, monkeypatch, streams):
         for msg, lo, hi in ((b"bradfitz", 0, 3_000_000), (M120, 10**19 - 1_500_000, 10**19 + 1_500_000)):
             assert c.search(msg, lo, hi) == oracle.search(msg, lo, hi, threads=8)
         assert c.search(bytes.fromhex(c2["msg_hex"]), c2["lower"], c2["upper"]) == (c2["hash"], c2["nonce"])
+
+
+@pytest.mark.parametrize("tail", [0, 1, 99_991, 1 << 24])
+def test_tail_launch_split(oracle, monkeypatch, tail):
+    """The biggest launch's last BTCMINER_TAIL nonces run as a launch of their
+    own (10-nonce tasks) when there are streams to overlap on: the split at
+    any size, including 1 nonce and a prime, leaves every answer unchanged."""
+    from distributed_bitcoin_minter_amd import Context
+    monkeypatch.setenv("BTCMINER_TAIL", str(tail))
+    c2 = next(c for c in load_golden("full_range.json")["cases"] if c["config"] == "C2")
+    with Context(devices=[0]) as c:
+        for msg, lo, hi in ((b"bradfitz", 0, 3_000_000), (M120, 2**64 - 2_000_000, 2**64 - 1)):
+            assert c.search(msg, lo, hi) == oracle.search(msg, lo, hi, threads=8)
+        assert c.search(bytes.fromhex(c2["msg_hex"]), c2["lower"], c2["upper"]) == (c2["hash"], c2["nonce"])
