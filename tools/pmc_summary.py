@@ -28,7 +28,14 @@ for k, disp in per.items():
     if "search_kernel" not in k:
         continue
     acc, n = collections.defaultdict(list), collections.Counter()
+    # main launches only: one template can also run a short tail launch per
+    # call, which averaging would mix in
+    top = collections.defaultdict(float)
+    for d in disp:
+        top[d[0]] = max(top[d[0]], dur[k][d])
     for d, cs in disp.items():
+        if dur[k][d] <= 0.5 * top[d[0]]:
+            continue
         for c, v in cs.items():
             acc[c].append(v)
         acc["_dur_s"].append(dur[k][d])
