@@ -70,7 +70,11 @@ int bm_device_count(int* out);
 
 /* Context over devices 0..num_gpus-1 (num_gpus = 0: all visible devices).
  * A context with several devices splits every search across them and
- * combines the per-device 16-byte partials with one RCCL allgather. */
+ * combines the per-device 16-byte partials with one RCCL allgather.
+ * Launch-overlap tuning is read from the environment at creation (results
+ * never depend on it): BTCMINER_STREAMS = launch streams per device (1..4,
+ * default 2); BTCMINER_TAIL = nonces split off the biggest launch into a
+ * short-task launch of their own (default 16777216, 0 = off). */
 int bm_ctx_create(int num_gpus, bm_ctx_t** out);
 /* Context over an explicit device list (e.g. {LOCAL_RANK} for one process
  * per GPU). */
