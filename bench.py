@@ -1,67 +1,142 @@
 #!/usr/bin/env python3
 """Benchmark of the nonce-search hot path (BASELINE.json metric: GH/s of the
-SHA-256 "msg nonce" min-search, and its fraction of the int32 VALU roofline).
+SHA-256 "msg nonce" min-search at 1/2/4/8 MI355X, and its fraction of the
+int32 VALU roofline).
 
-Workload = BASELINE config C2 (configs[1]): msg "bradfitz", nonces
-[0, 2^32-1] on one MI355X, bit-exact min (hash, nonce).  With --gpus N
-(torchrun, one process per GPU) the scaling is WEAK: rank r searches
-[r*2^32, (r+1)*2^32 - 1] on its own GPU, and the 16-byte partials are
-combined with one all_gather over RCCL (the only exchange the path has).
+Workloads (--config):
+  C2 (default, BASELINE configs[1])  msg "bradfitz", 2^32 nonces per GPU:
+      [0, N*2^32-1] over N GPUs, rank/device r scanning [r*2^32, (r+1)*2^32-1]
+      (weak scaling; at N = 1 exactly C2's [0, 2^32-1]).
+  C3 (configs[2])  the 120-byte message, 20-digit nonces:
+      [2^64 - N*2^32, 2^64-1] (weak scaling).
+  C4 (configs[3])  msg "bradfitz", [0, 2^40-1] split over the N GPUs
+      (strong scaling; about 20 s per step on one GPU).
 
-A step = one complete search (all kernel launches, the second-pass
-reduction, the 16-byte result copy) of every rank's 2^32 nonces plus the
-combine.  value = total nonces of all ranks / max-over-ranks step time.
+How N GPUs are driven (--gpus N):
+  * torchrun (WORLD_SIZE = N > 1, the driver's multi-GPU launch): one process
+    per GPU.  Each rank opens a library context that is one rank of an RCCL
+    group (bm_ctx_create_rank on LOCAL_RANK; rank 0's unique id travels over
+    the rendezvous), every rank calls bm_search_gpu on the WHOLE range, scans
+    its contiguous piece, and one RCCL allgather of the 16-byte partials gives
+    every rank the answer.  torch.distributed (gloo, CPU) runs only in a
+    sidecar process (distributed_bitcoin_minter_amd/rendezvous.py) for the
+    unique id, the barriers and the max over ranks, so this process maps one
+    HIP runtime, /opt/rocm's, the one the GPU test suite runs on.
+  * no launcher, N > 1: ONE process drives N devices (BASELINE C4's design):
+    a multi-device context splits the range and combines with
+    ncclCommInitAll + ncclAllGather inside the library.  Fewer than N visible
+    devices is an error, unless --rehearse-one-gpu (every "device" is GPU 0,
+    partials combined on the host: checks the N-way split, not a measurement).
+  * N = 1: one device, no collective.
+
+A step = one complete bm_search_gpu over the workload (every kernel launch,
+the second-pass reduction, the combine, the 16-byte result copy); the call is
+synchronous, so the step boundary is a device synchronisation.  Timed region:
+barrier -> K steps -> barrier, max over ranks.  value = all nonces of all
+ranks / that time.  The answer is checked against the committed golden
+(tests/golden/) for the workload; a wrong answer exits non-zero.
 
 Also reported:
-  roofline      dominant launch (the 10-digit segment) : algorithmic int32
-                ops (nonces x C x 1384) / its HIP-event time
-                on the library's stream, vs 78.64 T lane-ops/s per GPU.
-  cpu_baseline  the CPU oracle's loop shape (format + SHA-256 + strict '<',
-                OpenSSL block code) on this host's cores over a bounded
-                sample of the same workload (rank 0, N = 1 only); and, under
-                "system", the reference's deployment on the same cores: one
-                LSP server + N single-threaded CPU miner processes + a client
-                over the same window, its answer checked against the oracle.
+  roofline      the dominant launch: algorithmic int32 ops (nonces x C x 1384,
+                SURVEY.md §8d, C = SHA-256 blocks the kernel compresses per
+                nonce) / its HIP-event time on the library's stream, vs 78.64 T
+                lane-ops/s per GPU; PMC figures (VALU per nonce, clock under
+                the kernel, memory-side bytes) from profiles/<round>/ for the
+                same config.
+  cpu_baseline  the oracle's loop shape (format + SHA-256 + strict '<') on this
+                host's cores over a bounded sample of C2 (rank 0, N = 1 only);
+                "system": one LSP server + N single-threaded CPU miner processes
+                + a client over the same window.
 """
 import argparse
+import glob
 import json
 import os
 import sys
 import time
 
-# torch first: libbtcminer.so then binds to torch's HIP runtime, so the
-# process holds exactly one (see tests/conftest.py).
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from distributed_bitcoin_minter_amd import Context  # noqa: E402
-from distributed_bitcoin_minter_amd.dist import combine  # noqa: E402
+from distributed_bitcoin_minter_amd import _lib  # noqa: E402
+from distributed_bitcoin_minter_amd._lib import Context, device_count, rccl_unique_id  # noqa: E402
+from distributed_bitcoin_minter_amd.dist import lex_min, rank_piece  # noqa: E402
 
-MSG = b"bradfitz"
+U64 = (1 << 64) - 1
 PER_GPU = 1 << 32
+MSG_C2 = b"bradfitz"
+M120 = (b"The quick brown fox jumps over the lazy dog. " * 3)[:120]
 VALU_PEAK_T = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.64 T int32 lane-ops/s (MI355X_MICROARCH.md)
 OPS_PER_COMPRESSION = 1384                  # canonical int32 VALU ops
+METRIC = "GH/s (SHA-256 \"msg nonce\" min-search) at 1/2/4/8 MI355X; % of int32 VALU peak"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def workload(config, n):
+    """(msg, lower, upper, scaling, description) of a config at n GPUs."""
+    if config == "C2":
+        return (MSG_C2, 0, n * PER_GPU - 1, "weak",
+                "C2: msg 'bradfitz', nonces [0, N*2^32-1], 2^32 per GPU (GPU r: [r*2^32, (r+1)*2^32-1]), "
+                "inclusive min (hash, nonce)")
+    if config == "C3":
+        return (M120, U64 - n * PER_GPU + 1, U64, "weak",
+                "C3: 120-byte msg, 20-digit nonces [2^64 - N*2^32, 2^64-1], 2^32 per GPU, inclusive min (hash, nonce)")
+    if config == "C4":
+        return (MSG_C2, 0, (1 << 40) - 1, "strong",
+                "C4: msg 'bradfitz', nonces [0, 2^40-1] split over the N GPUs, inclusive min (hash, nonce)")
+    raise ValueError(config)
+
+
+def golden(msg, lo, hi):
+    """The committed answer for (msg, [lo, hi]), or None."""
+    gdir = os.path.join(ROOT, "tests", "golden")
+    cands = []
+    for name in ("full_range.json", "scale_ranges.json"):
+        try:
+            d = json.load(open(os.path.join(gdir, name)))
+        except (OSError, ValueError):
+            continue
+        cands += d.get("cases", []) + [dict(r, msg_hex=d["msg_hex"]) for r in d.get("ranges", [])]
+    for c in cands:
+        if bytes.fromhex(c["msg_hex"]) == msg and c["lower"] == lo and c["upper"] == hi:
+            return [c["hash"], c["nonce"]]
+    return None
+
+
 def compressions_per_nonce(msg_len, digits):
-    """C(L, D) = ceil((L+D+10)/64) - floor((L+1)/64)."""
+    """Survey C(L, D) = ceil((L+D+10)/64) - floor((L+1)/64):
+    whole prefix blocks only counted as midstate."""
     return -(-(msg_len + digits + 10) // 64) - (msg_len + 1) // 64
 
 
-def issue_bound(p, nbv=1, clock_ghz=2.37):
+def pmc_summary(config, p, nbv=1):
+    """The newest committed rocprofv3 PMC summary entry for search_kernel<p, nbv>
+    under this config (tools/pmc_summary.py: main launches only); PMC passes
+    cannot run inside this timed process."""
+    pats = [f"pmc_summary_{config}.json"] + (["pmc_summary.json"] if config == "C2" else [])
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary*.json")), reverse=True):
+        if os.path.basename(path) not in pats:
+            continue
+        try:
+            summ = json.load(open(path))
+        except ValueError:
+            continue
+        for k, e in summ.items():
+            if f"search_kernel<{p}, {nbv}>" in k:
+                return e, os.path.relpath(path, ROOT)
+    return None, None
+
+
+def issue_bound(p, nbv, clock_ghz):
     """gfx950 VALU issue bound of the kernel's inner loop: each
     slow op (v_alignbit, v_add3, SGPR operand, ...) takes an issue slot of its
     own, fast ops of two waves share one, so a SIMD needs max(slow, (slow +
     fast) / 2) slots of 4 cycles per 64 nonces; static counts from
-    tools/isa_mix.py on the built assembly, clock as measured under this
-    kernel (GRBM_GUI_ACTIVE, profiles/r01)."""
+    tools/isa_mix.py on the built assembly, at the clock PMC measured under
+    this kernel."""
     path = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc", "isa_mix.json")
     try:
         lay = json.load(open(path))["layouts"][f"{p}:{nbv}"]
@@ -70,23 +145,17 @@ def issue_bound(p, nbv=1, clock_ghz=2.37):
     cyc = lay["simd_cycles_per_64_nonces"]
     ghs = 256 * 4 * clock_ghz * 1e9 * 64 / cyc / 1e9
     return {"valu_per_nonce": lay["valu"], "slow": lay["valu_slow"], "fast": lay["valu_fast"],
-            "issue_slots_per_nonce": lay["issue_slots"], "clock_ghz": clock_ghz, "GHs_per_gpu": round(ghs, 2)}
+            "issue_slots_per_nonce": lay["issue_slots"], "clock_ghz": round(clock_ghz, 3),
+            "GHs_per_gpu": round(ghs, 2)}
 
 
-def pmc_traffic(p, nbv=1):
-    """HBM bytes per launch of search_kernel<p, nbv> from the newest committed
-    rocprofv3 PMC summary (FETCH_SIZE + WRITE_SIZE passes, tools/pmc_summary.py);
-    PMC passes cannot run inside this timed process."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), reverse=True):
-        try:
-            summ = json.load(open(path))
-        except ValueError:
-            continue
-        for k, e in summ.items():
-            if f"search_kernel<{p}, {nbv}>" in k and "hbm_bytes_per_launch" in e:
-                return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT), e.get("counters", {})
-    return None, None, {}
+def hip_runtimes():
+    """HIP runtime libraries mapped into this process."""
+    try:
+        maps = open("/proc/self/maps").read().splitlines()
+    except OSError:
+        return None
+    return sorted({ln.split()[-1] for ln in maps if "libamdhip64" in ln})
 
 
 def cpu_baseline(target_s=10.0):
@@ -103,11 +172,11 @@ def cpu_baseline(target_s=10.0):
     hi = PER_GPU - 1
     n = 1 << 21
     t = time.perf_counter()
-    oracle.search(MSG, hi - n + 1, hi, threads=threads, openssl=True)
+    oracle.search(MSG_C2, hi - n + 1, hi, threads=threads, openssl=True)
     rate = n / (time.perf_counter() - t)
     n = int(min(PER_GPU, max(n, rate * target_s)))
     t = time.perf_counter()
-    want = oracle.search(MSG, hi - n + 1, hi, threads=threads, openssl=True)
+    want = oracle.search(MSG_C2, hi - n + 1, hi, threads=threads, openssl=True)
     dt = time.perf_counter() - t
     out = {"value": n / dt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port",
            "sample": f"msg 'bradfitz', last {n} nonces of [0, 2^32-1] (10-digit, 1 SHA-256 block each), "
@@ -163,7 +232,7 @@ def cpu_system_baseline(lib, n_miners, lo, hi, want, chunk_bits=24):
                 raise RuntimeError(f"only {bs.stats['joins']} of {n_miners} CPU miners joined")
             time.sleep(0.05)
         t = time.perf_counter()
-        got = client.request(hostport, MSG.decode(), hi, p, lower=lo)
+        got = client.request(hostport, MSG_C2.decode(), hi, p, lower=lo)
         dt = time.perf_counter() - t
     finally:
         bs.close()
@@ -178,127 +247,187 @@ def cpu_system_baseline(lib, n_miners, lo, hi, want, chunk_bits=24):
                       f"localhost, msg 'bradfitz', nonces [{lo}, {hi}], 2^{chunk_bits}-nonce chunks"}
 
 
+class Group:
+    """Barrier / max / gather across the ranks of this run (one process: trivial)."""
+
+    def __init__(self, rdzv=None):
+        self.rdzv = rdzv
+        self.rank = rdzv.rank if rdzv else 0
+        self.world = rdzv.world if rdzv else 1
+
+    def barrier(self):
+        if self.rdzv:
+            self.rdzv.barrier()
+
+    def max(self, x):
+        return self.rdzv.all_max(x) if self.rdzv else x
+
+    def gather(self, obj):
+        return self.rdzv.all_gather(obj) if self.rdzv else [obj]
+
+    def close(self):
+        if self.rdzv:
+            self.rdzv.close()
+
+
+def open_contexts(args, world, rank, local):
+    """(ctx, group, search, parallelism) for the launch mode (module docstring)."""
+    if world > 1:
+        from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
+        grp = Group(Rendezvous())
+        if args.rehearse_one_gpu or args.combine == "gloo":
+            # every rank scans its piece on its own context; the 16-byte
+            # partials are gathered over the gloo sidecar
+            dev = 0 if args.rehearse_one_gpu else local
+            ctx = Context(devices=[dev])
+
+            def search(msg, lo, hi):
+                piece = rank_piece(lo, hi, grp.rank, grp.world)
+                part = ctx.search(msg, *piece) if piece else (U64, U64)
+                return lex_min(tuple(p) for p in grp.gather(list(part)))
+            how = f"{world} processes (one per GPU), gloo gather of 16 B partials"
+            if args.rehearse_one_gpu:
+                how += " [rehearsal: every rank on GPU 0]"
+            return ctx, grp, search, how
+        uid = grp.rdzv.broadcast_bytes(rccl_unique_id() if grp.rank == 0 else None)
+        ctx = Context(devices=[local], rank=grp.rank, world=grp.world, unique_id=uid)
+        return ctx, grp, ctx.search, f"{world} processes (one per GPU), RCCL allgather of 16 B partials in-library"
+    grp = Group()
+    n = args.gpus
+    if n > 1:
+        if args.rehearse_one_gpu:
+            ctx = Context(devices=[0] * n)  # same device n times: host combine
+            return ctx, grp, ctx.search, f"one process, {n}-way split on GPU 0 [rehearsal], host combine"
+        have = device_count()
+        if have < n:
+            log(f"error: --gpus {n} but only {have} HIP device(s) visible "
+                "(use torchrun for one process per GPU, or --rehearse-one-gpu to check the split on one GPU)")
+            sys.exit(2)
+        ctx = Context(num_gpus=n)
+        return ctx, grp, ctx.search, f"one process, {n} devices, RCCL ncclAllGather of 16 B partials in-library"
+    ctx = Context(devices=[local])
+    return ctx, grp, ctx.search, "1 device"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4"])
+    ap.add_argument("--combine", default="rccl", choices=["rccl", "gloo"],
+                    help="torchrun ranks: in-library RCCL allgather (default) or gather over the gloo sidecar")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
-                    help="N>1 ranks on ONE GPU (every rank uses device 0, gloo combine on CPU): "
-                         "exercises the multi-rank path on a one-GPU box; not a scaling measurement")
+                    help="N-way split on ONE GPU (all ranks / devices are GPU 0): exercises the multi-GPU "
+                         "path on a one-GPU box; not a scaling measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    if args.rehearse_one_gpu:
-        local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        if args.rehearse_one_gpu:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
-    cdev = torch.device("cpu") if args.rehearse_one_gpu else dev
+    if world > 1 and args.gpus != world:
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}")
+        sys.exit(2)
+    _lib.load()  # before anything else can map a second HIP runtime
 
-    lo = rank * PER_GPU
-    hi = lo + PER_GPU - 1
-    ctx = Context(devices=[local])
+    ctx, grp, search, how = open_contexts(args, world, rank, local)
     ctx.set_timing(True)
+    n = args.gpus
+    msg, lo, hi, scaling, desc = workload(args.config, n)
 
     def step():
-        part = ctx.search(MSG, lo, hi)
-        dom = None
+        res = search(msg, lo, hi)
         st = ctx.last_stats()
-        for i in range(st.recorded):
-            L = st.launch[i]
-            if dom is None or L.nonces > dom.nonces:
-                dom = L
-        res = combine(part, device=cdev) if world > 1 else part
-        return res, (dom.nonces, dom.ms, dom.digits, dom.p, dom.grid, dom.tasks_per_thread, dom.inner_digits)
+        dom = max((st.launch[i] for i in range(st.recorded)), key=lambda L: L.nonces, default=None)
+        return res, dom
 
     for _ in range(args.warmup):
-        res, _ = step()
-
-    def sync():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    sync()
+        step()
+    grp.barrier()
     t0 = time.perf_counter()
     doms = []
+    res = None
     for _ in range(args.steps):
         res, d = step()
         doms.append(d)
-    sync()
     dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = tt.item()
+    grp.barrier()
+    dt = grp.max(dt)
 
-    total = PER_GPU * world * args.steps
-    value = total / dt / 1e9
-    dom_nonces, _, dom_digits, dom_p, dom_grid, dom_tpt, dom_inner = doms[-1]
-    dom_ms = sum(d[1] for d in doms) / len(doms)
-    C = compressions_per_nonce(len(MSG), dom_digits)
-    achieved = dom_nonces * C * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
-    mix = issue_bound(dom_p)
-    traffic, traffic_src, pmc = pmc_traffic(dom_p)
-    # measured VALU per nonce (SQ_INSTS_VALU counts wave-instructions: x64 lanes)
-    valu_pmc = pmc["SQ_INSTS_VALU"] * 64 / dom_nonces if "SQ_INSTS_VALU" in pmc else None
-    # fraction of VALU instructions issued as the second of a same-cycle pair (PMC)
-    valu2 = pmc["SQ_ACTIVE_INST_VALU2"] / pmc["SQ_INSTS_VALU"] if "SQ_ACTIVE_INST_VALU2" in pmc else None
-    check = None
-    if world == 1:
-        check = list(res)  # C2 golden: (5256245051, 1626825724)
-
+    total = hi - lo + 1
+    value = total * args.steps / dt / 1e9
+    want = golden(msg, lo, hi)
+    dom = doms[-1]
     out = {
-        "metric": "GH/s (SHA-256 \"msg nonce\" min-search) at 1/2/4/8 MI355X; % of int32 VALU peak",
+        "metric": METRIC,
         "value": round(value, 4),
         "unit": "GH/s",
-        "n_gpus": world,
+        "n_gpus": n,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": "C2: msg 'bradfitz', nonces [0, 2^32-1] per GPU (rank r: [r*2^32, (r+1)*2^32-1]), "
-                               "inclusive min (hash, nonce)",
-                   "msg": MSG.decode(), "nonces_per_gpu": PER_GPU, "global_nonces": PER_GPU * world,
-                   "parallelism": f"range-split x{world}" + (", RCCL all_gather of 16 B partials" if world > 1 else "")},
-        "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_T, 2),
-                     "unit": "T int32 lane-ops/s", "frac": round(achieved / VALU_PEAK_T, 4), "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE+WRITE_SIZE)", "traffic_src": traffic_src,
-                     "traffic_note": "the per-launch dequeue counter's returning atomics (64-B memory-side "
-                                     "requests); the search reads no input from HBM (DESIGN.md §5)",
-                     "valu_per_nonce_pmc": valu_pmc and round(valu_pmc, 1),
-                     "valu_dual_issued_frac_pmc": valu2 and round(valu2, 4),
-                     "kernel": f"search_kernel<P={dom_p},NBV=1> ({dom_digits}-digit nonces)",
-                     "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom_nonces,
-                     "ops_per_nonce": C * OPS_PER_COMPRESSION, "grid": dom_grid,
-                     "tasks_per_thread": dom_tpt, "inner_digits": dom_inner,
-                     "issue_bound": mix and dict(mix, frac=round(dom_nonces / (dom_ms * 1e-3) / 1e9
-                                                                  / mix["GHs_per_gpu"], 4))},
-        "result": check,
+        "config": {"workload": desc, "name": args.config, "msg": msg.decode(), "lower": lo, "upper": hi,
+                   "global_nonces": total, "parallelism": how},
+        "result": list(res),
+        "golden": want,
+        "result_ok": None if want is None else list(res) == want,
+        "hip_runtime": hip_runtimes(),
     }
+    if dom is not None:
+        ms = [d.ms for d in doms if d is not None]
+        dom_ms = sum(ms) / len(ms)
+        c_eff = dom.nbv + dom.pad_block  # blocks the kernel compresses per nonce
+        c_survey = compressions_per_nonce(len(msg), dom.digits)
+        achieved = dom.nonces * c_eff * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
+        pmc, pmc_src = pmc_summary(args.config, dom.p, dom.nbv)
+        pmc = pmc or {}
+        cnt = pmc.get("counters", {})
+        clock = pmc.get("clock_ghz")
+        roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_T, 2),
+                "unit": "T int32 lane-ops/s", "frac": round(achieved / VALU_PEAK_T, 4),
+                "traffic": pmc.get("hbm_bytes_per_launch"),
+                "traffic_unit": "memory-side bytes per launch (PMC FETCH_SIZE+WRITE_SIZE)",
+                "traffic_note": "the per-launch dequeue counter's returning atomics; the search reads no input "
+                                "from HBM (DESIGN.md §5)",
+                "pmc_src": pmc_src,
+                "kernel": f"search_kernel<P={dom.p},NBV={dom.nbv}> ({dom.digits}-digit nonces)",
+                "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom.nonces,
+                "compressions_per_nonce": c_eff, "ops_per_nonce": c_eff * OPS_PER_COMPRESSION,
+                "grid": dom.grid, "tasks_per_thread": dom.tasks_per_thread, "inner_digits": dom.inner_digits}
+        if c_survey != c_eff:
+            # SURVEY §8d counts only whole prefix blocks as midstate; the planner
+            # also folds constant high digits, so the kernel does less work
+            roof["survey_compressions_per_nonce"] = c_survey
+            roof["survey_frac"] = round(dom.nonces * c_survey * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
+                                        / VALU_PEAK_T, 4)
+        if "SQ_INSTS_VALU" in cnt:  # wave-instructions: x64 lanes
+            roof["valu_per_nonce_pmc"] = round(cnt["SQ_INSTS_VALU"] * 64 / dom.nonces, 1)
+        if "SQ_ACTIVE_INST_VALU2" in cnt and cnt.get("SQ_INSTS_VALU"):
+            roof["valu_dual_issued_frac_pmc"] = round(cnt["SQ_ACTIVE_INST_VALU2"] / cnt["SQ_INSTS_VALU"], 4)
+        if clock:
+            roof["clock_ghz_pmc"] = round(clock, 3)
+            ib = issue_bound(dom.p, dom.nbv, clock)
+            if ib:
+                ib["frac"] = round(dom.nonces / (dom_ms * 1e-3) / 1e9 / ib["GHs_per_gpu"], 4)
+                roof["issue_bound"] = ib
+        out["roofline"] = roof
     if args.rehearse_one_gpu:
-        out["rehearsal"] = "all ranks on device 0, gloo combine: checks the multi-rank path, not a measurement"
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["rehearsal"] = "every rank / device is GPU 0: checks the multi-GPU split and combine, not a measurement"
+    if grp.rank == 0 and n == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
-    if rank == 0:
+    if grp.rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    grp.close()
+    if out["result_ok"] is False:
+        log(f"error: result {out['result']} != golden {want}")
+        sys.exit(1)
 
 
 if __name__ == "__main__":

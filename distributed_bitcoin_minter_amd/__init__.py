@@ -10,7 +10,8 @@ re-built as gfx950 HIP kernels behind the C ABI in include/btcminer.h
         print(m.search("bradfitz", 0, 9999))   # (1419516646206828, 9898)
 """
 from . import bitcoin, dist
-from ._lib import BtcMinerError, Context, LIB_PATH, device_count, plan_segments
+from ._lib import BtcMinerError, Context, LIB_PATH, device_count, plan_segments, rccl_unique_id
 from .miner import Miner
 
-__all__ = ["bitcoin", "dist", "Miner", "Context", "BtcMinerError", "LIB_PATH", "device_count", "plan_segments"]
+__all__ = ["bitcoin", "dist", "Miner", "Context", "BtcMinerError", "LIB_PATH", "device_count", "plan_segments",
+           "rccl_unique_id"]

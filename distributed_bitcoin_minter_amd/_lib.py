@@ -19,6 +19,8 @@ BM_ERCCL = -4
 BM_ENOMEM = -5
 BM_EINTERNAL = -6
 BM_MAX_LAUNCH_STATS = 64
+BM_RCCL_ID_BYTES = 128
+BM_ABI_VERSION = 2
 BM_COMBINE_AUTO, BM_COMBINE_RCCL, BM_COMBINE_HOST = 0, 1, 2
 U64_MAX = (1 << 64) - 1
 
@@ -39,7 +41,7 @@ class LaunchStat(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("launches", c_u32), ("recorded", c_u32), ("wall_ms", ctypes.c_double),
-                ("kernel_ms", ctypes.c_double), ("nonces", c_u64),
+                ("kernel_ms", ctypes.c_double), ("span_ms", ctypes.c_double), ("nonces", c_u64),
                 ("launch", LaunchStat * BM_MAX_LAUNCH_STATS)]
 
 
@@ -66,7 +68,11 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise OSError(f"{LIB_PATH} is missing: build it with `make -C {os.path.join(_HERE, 'csrc')} -j8` "
                       "(or __graft_entry__.build())")
-    lib = ctypes.CDLL(LIB_PATH)
+    # RTLD_NOW: every HIP/RCCL symbol of the library (and of the runtime it
+    # pulls in) binds at load time.  A process that imports torch afterwards
+    # maps torch's bundled HIP runtime too; lazy binding could then resolve
+    # some of our calls into that second runtime.
+    lib = ctypes.CDLL(LIB_PATH, mode=os.RTLD_NOW | os.RTLD_LOCAL)
     P = ctypes.POINTER
     vp = ctypes.c_void_p
     sigs = {
@@ -77,6 +83,11 @@ def load():
         "bm_ctx_create_devices": ([P(ctypes.c_int), ctypes.c_int, P(vp)], ctypes.c_int),
         "bm_ctx_destroy": ([vp], ctypes.c_int),
         "bm_ctx_num_devices": ([vp, P(ctypes.c_int)], ctypes.c_int),
+        "bm_rccl_unique_id": ([ctypes.c_char_p], ctypes.c_int),
+        "bm_ctx_create_rank": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, P(vp)], ctypes.c_int),
+        "bm_ctx_rank": ([vp, P(ctypes.c_int), P(ctypes.c_int)], ctypes.c_int),
+        "bm_reduce_gpu": ([vp, P(Result), ctypes.c_size_t, P(Result)], ctypes.c_int),
+        "bm_ctx_set_test_fault": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_search_gpu": ([vp, ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, P(Result)], ctypes.c_int),
         "bm_hash_gpu": ([vp, ctypes.c_char_p, ctypes.c_size_t, P(c_u64), ctypes.c_size_t, P(c_u64)],
                         ctypes.c_int),
@@ -95,6 +106,8 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
+    if lib.bm_abi_version() != BM_ABI_VERSION:
+        raise OSError(f"{LIB_PATH}: ABI version {lib.bm_abi_version()}, expected {BM_ABI_VERSION}; rebuild it")
     _lib = lib
     return lib
 
@@ -131,13 +144,31 @@ def plan_segments(msg: bytes, lower: int, upper: int, max_windows: int = DEFAULT
     return list(arr[: n.value])
 
 
-class Context:
-    """Owns a bm_ctx over one or more GPUs.  Not thread-safe (like the C ctx)."""
+def rccl_unique_id() -> bytes:
+    """RCCL unique id for a process group (rank 0 makes it, every rank
+    passes it to Context(rank=..., world=..., unique_id=...))."""
+    buf = ctypes.create_string_buffer(BM_RCCL_ID_BYTES)
+    check(load().bm_rccl_unique_id(buf), "bm_rccl_unique_id")
+    return buf.raw
 
-    def __init__(self, devices=None, num_gpus=0):
+
+class Context:
+    """Owns a bm_ctx over one or more GPUs.  Not thread-safe (like the C ctx).
+
+    Context(devices=[...]) / Context(num_gpus=N): one process, N devices.
+    Context(devices=[d], rank=r, world=w, unique_id=uid): rank r of an RCCL
+    process group (one process per GPU); blocks until all w ranks join."""
+
+    def __init__(self, devices=None, num_gpus=0, rank=None, world=None, unique_id=None):
         lib = load()
         h = ctypes.c_void_p()
-        if devices is not None:
+        if world is not None:
+            if devices is None or len(devices) != 1 or rank is None or unique_id is None:
+                raise ValueError("a rank context takes devices=[device], rank, world and unique_id")
+            if len(unique_id) != BM_RCCL_ID_BYTES:
+                raise ValueError(f"unique_id must be {BM_RCCL_ID_BYTES} bytes")
+            check(lib.bm_ctx_create_rank(devices[0], rank, world, unique_id, ctypes.byref(h)), "bm_ctx_create_rank")
+        elif devices is not None:
             ids = (ctypes.c_int * len(devices))(*devices)
             check(lib.bm_ctx_create_devices(ids, len(devices), ctypes.byref(h)), "bm_ctx_create_devices")
         else:
@@ -172,6 +203,24 @@ class Context:
         n = ctypes.c_int(0)
         check(self._lib.bm_ctx_num_devices(self.handle, ctypes.byref(n)), "bm_ctx_num_devices")
         return n.value
+
+    def rank(self):
+        """(rank, world) of the context's process group ((0, 1) if none)."""
+        r, w = ctypes.c_int(0), ctypes.c_int(0)
+        check(self._lib.bm_ctx_rank(self.handle, ctypes.byref(r), ctypes.byref(w)), "bm_ctx_rank")
+        return r.value, w.value
+
+    def reduce(self, pairs):
+        """Lexicographic min of (hash, nonce) pairs by the GPU reductions
+        (bm_reduce_gpu, a test entry)."""
+        n = len(pairs)
+        arr = (Result * max(n, 1))(*[Result(h, nn) for h, nn in pairs])
+        r = Result()
+        check(self._lib.bm_reduce_gpu(self.handle, arr, n, ctypes.byref(r)), "bm_reduce_gpu")
+        return r.hash, r.nonce
+
+    def set_test_fault(self, launches: int):
+        check(self._lib.bm_ctx_set_test_fault(self.handle, launches), "bm_ctx_set_test_fault")
 
     def search(self, msg: bytes, lower: int, upper: int):
         """Inclusive [lower, upper] min-scan -> (hash, nonce)."""

@@ -92,15 +92,35 @@ class Message:
 
     @classmethod
     def unmarshal(cls, raw) -> "Message":
-        """json.Unmarshal into a Message: absent fields keep zero values."""
-        d = json.loads(raw)
-        m = cls(Type=MsgType(int(d.get("Type", 0))), Data=d.get("Data", "") or "",
-                Lower=int(d.get("Lower", 0)), Upper=int(d.get("Upper", 0)),
-                Hash=int(d.get("Hash", 0)), Nonce=int(d.get("Nonce", 0)))
-        for f in ("Lower", "Upper", "Hash", "Nonce"):
-            if not 0 <= getattr(m, f) <= U64_MAX:
-                raise ValueError(f"{f} out of uint64 range")
-        return m
+        """json.Unmarshal into a Message: absent (or null) fields keep zero
+        values; a field of the wrong JSON type is an error, as in Go (Data a
+        string; Type an int; Lower/Upper/Hash/Nonce integers in uint64 range,
+        no floats, no booleans).  Anything else raises ValueError."""
+        try:
+            d = json.loads(raw)
+        except (UnicodeDecodeError, RecursionError) as e:
+            raise ValueError(f"not a JSON message: {e!r}") from None
+        if not isinstance(d, dict):
+            raise ValueError("bitcoin message is not a JSON object")
+
+        def num(f, lo, hi):
+            v = d.get(f)
+            if v is None:
+                return 0
+            if isinstance(v, bool) or not isinstance(v, int):
+                raise ValueError(f"{f} is not an integer")
+            if not lo <= v <= hi:
+                raise ValueError(f"{f} out of range")
+            return v
+
+        data = d.get("Data")
+        if data is None:
+            data = ""
+        if not isinstance(data, str):
+            raise ValueError("Data is not a string")
+        return cls(Type=MsgType(num("Type", -(1 << 63), (1 << 63) - 1)), Data=data,
+                   Lower=num("Lower", 0, U64_MAX), Upper=num("Upper", 0, U64_MAX),
+                   Hash=num("Hash", 0, U64_MAX), Nonce=num("Nonce", 0, U64_MAX))
 
     def String(self) -> str:
         """message.go:49-60."""

@@ -1,6 +1,7 @@
 // bm_api.hip -- C ABI of libbtcminer.so (include/btcminer.h): device
 // contexts, launch sizing, the per-device reduction and the multi-GPU
-// RCCL allgather of 16-byte partials.
+// RCCL allgather of 16-byte partials (one process over N devices, or one
+// process per device joined into an RCCL communicator).
 //
 // Drop-in for the reference miner's job loop body: miner.go:58-65 calls
 // bitcoin.Hash (hash.go:11-15) once per nonce and keeps a strict-'<' minimum;
@@ -9,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -33,6 +35,7 @@ constexpr int kEventPairs = BM_MAX_LAUNCH_STATS;
 // call go out biggest first over the streams, and the next launch's
 // workgroups fill the CUs the previous one frees.
 constexpr int kMaxStreams = 4;
+constexpr uint64_t kMaxTailNonces = 1ull << 40;
 
 struct DeviceCtx {
     int id = -1;
@@ -43,14 +46,16 @@ struct DeviceCtx {
     unsigned long long* d_ctr = nullptr;  // one dequeue counter per launch
     size_t ctr_cap = 0;
     Partial* d_result = nullptr;  // 1 partial
-    Partial* d_gather = nullptr;  // n_dev partials (allgather target)
-    Partial* h_result = nullptr;  // pinned, n_dev partials
+    Partial* d_gather = nullptr;  // nslots partials (allgather target)
+    Partial* h_result = nullptr;  // pinned, nslots partials
+    Partial* d_test = nullptr;    // bm_reduce_gpu's staging buffer
+    size_t test_cap = 0;
     uint64_t* d_hash_io = nullptr;
     size_t hash_cap = 0;
     hipEvent_t ev[2 * kEventPairs] = {};
     hipStream_t aux[kMaxStreams - 1] = {};  // extra launch streams (ctx->streams > 1)
     hipEvent_t fork = nullptr, join[kMaxStreams - 1] = {};
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;  // multi-device ctx: ncclCommInitAll; rank ctx: the process group's
     std::vector<std::pair<const void*, int>> occ;  // kernel -> blocks per CU
 };
 
@@ -94,6 +99,8 @@ struct bm_ctx {
     uint64_t tail_nonces = 1ull << 24;  // split off the biggest launch's last nonces (BTCMINER_TAIL; 0: off; profiles/r01/ab_tail.log)
     int streams = 2;      // launch streams per device (1..kMaxStreams; BTCMINER_STREAMS; profiles/r01/ab_streams.log)
     bool nccl_ready = false;
+    int rank = 0, world = 1;  // bm_ctx_create_rank: this process's place in an RCCL process group
+    int fault_after = -1;     // test hook: fail after enqueueing this many launches (-1: off)
     bm_stats_t stats;
 };
 
@@ -204,7 +211,9 @@ int ensure_partials(DeviceCtx& d, size_t n) {
     return BM_OK;
 }
 
-int init_device(DeviceCtx& d, int id, int ndev) {
+// nslots: partials the combine gathers (devices of the ctx, or ranks of its
+// process group).
+int init_device(DeviceCtx& d, int id, int nslots) {
     d.id = id;
     BM_HIP(hipSetDevice(id));
     hipDeviceProp_t prop;
@@ -213,8 +222,8 @@ int init_device(DeviceCtx& d, int id, int ndev) {
     d.cus = prop.multiProcessorCount;
     BM_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     BM_HIP(hipMalloc(&d.d_result, sizeof(Partial)));
-    BM_HIP(hipMalloc(&d.d_gather, sizeof(Partial) * (size_t)ndev));
-    BM_HIP(hipHostMalloc(&d.h_result, sizeof(Partial) * (size_t)ndev, hipHostMallocDefault));
+    BM_HIP(hipMalloc(&d.d_gather, sizeof(Partial) * (size_t)nslots));
+    BM_HIP(hipHostMalloc(&d.h_result, sizeof(Partial) * (size_t)nslots, hipHostMallocDefault));
     for (auto& e : d.ev) BM_HIP(hipEventCreate(&e));
     for (auto& s : d.aux) BM_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     BM_HIP(hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
@@ -238,6 +247,7 @@ void destroy_device(DeviceCtx& d) {
     if (d.d_result) (void)hipFree(d.d_result);
     if (d.d_gather) (void)hipFree(d.d_gather);
     if (d.d_hash_io) (void)hipFree(d.d_hash_io);
+    if (d.d_test) (void)hipFree(d.d_test);
     if (d.h_result) (void)hipHostFree(d.h_result);
     for (auto& e : d.join)
         if (e) (void)hipEventDestroy(e);
@@ -247,8 +257,18 @@ void destroy_device(DeviceCtx& d) {
     if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
+bool distinct_devices(const bm_ctx* ctx) {
+    for (size_t i = 0; i < ctx->devs.size(); ++i)
+        for (size_t j = 0; j < i; ++j)
+            if (ctx->devs[i].id == ctx->devs[j].id) return false;
+    return true;
+}
+
 int ensure_nccl(bm_ctx* ctx) {
     if (ctx->nccl_ready) return BM_OK;
+    // an RCCL communicator holds one rank per GPU: a device listed twice
+    // (a one-GPU rehearsal of the N-device split) combines on the host
+    if (!distinct_devices(ctx)) return BM_EINVAL;
     const int n = (int)ctx->devs.size();
     std::vector<ncclComm_t> comms(n);
     std::vector<int> ids(n);
@@ -256,6 +276,117 @@ int ensure_nccl(bm_ctx* ctx) {
     if (ncclCommInitAll(comms.data(), n, ids.data()) != ncclSuccess) return BM_ERCCL;
     for (int i = 0; i < n; ++i) ctx->devs[i].comm = comms[i];
     ctx->nccl_ready = true;
+    return BM_OK;
+}
+
+// Waits for everything a call may have queued on any stream of the context.
+// Used when a call fails part-way: launches already on the aux streams keep
+// running against d_ctr / d_part, so the next call (whose counter memset is
+// ordered only on the main stream) must not start before they end.
+void drain(bm_ctx* ctx) {
+    for (auto& d : ctx->devs) {
+        if (hipSetDevice(d.id) != hipSuccess) continue;
+        (void)hipStreamSynchronize(d.stream);
+        for (auto& s : d.aux)
+            if (s) (void)hipStreamSynchronize(s);
+    }
+    (void)hipGetLastError();
+}
+
+// Stages 2-3 of a search: enqueue every launch and the second-pass
+// reduction, combine the partials, wait.  On failure the caller drains.
+int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches, std::vector<uint32_t>& first,
+                        Partial* best_out) {
+    const int ndev = (int)ctx->devs.size();
+    int enqueued = 0;
+    for (int di = 0; di < ndev; ++di) {
+        DeviceCtx& d = ctx->devs[di];
+        BM_HIP(hipSetDevice(d.id));
+        uint32_t nparts = 0, li = 0;
+        if (!launches[di].empty())
+            BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches[di].size() * sizeof(unsigned long long), d.stream));
+        // stream of each launch: biggest first, round-robin over the streams
+        const int ns = std::max(1, std::min<int>(ctx->streams, (int)launches[di].size()));
+        std::vector<uint32_t> order(launches[di].size());
+        for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
+        if (ns > 1) {
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+                return launches[di][a].stat.nonces > launches[di][b].stat.nonces;
+            });
+            BM_HIP(hipEventRecord(d.fork, d.stream));
+            for (int k = 0; k + 1 < ns; ++k) BM_HIP(hipStreamWaitEvent(d.aux[k], d.fork, 0));
+        }
+        if (!order.empty()) first[di] = order[0];
+        for (uint32_t r = 0; r < order.size(); ++r) {
+            li = order[r];
+            Launch& L = launches[di][li];
+            hipStream_t s = (r % ns) == 0 ? d.stream : d.aux[r % ns - 1];
+            if (ctx->fault_after >= 0 && enqueued == ctx->fault_after) return BM_EINTERNAL;  // test hook
+            const bool timed = ctx->timing && li < (uint32_t)kEventPairs;
+            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li], s));
+            unsigned long long* ctr = d.d_ctr + li;
+            void* kargs[] = {&L.args, &d.d_part, &ctr};
+            BM_HIP(hipLaunchKernel(L.fn, dim3(L.grid), dim3(kBlock), kargs, 0, s));
+            ++enqueued;
+            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li + 1], s));
+            nparts += L.grid;
+        }
+        for (int k = 0; k + 1 < ns; ++k) {
+            BM_HIP(hipEventRecord(d.join[k], d.aux[k]));
+            BM_HIP(hipStreamWaitEvent(d.stream, d.join[k], 0));
+        }
+        // nparts = 0 (a device or rank with nothing to scan) writes (2^64-1, 2^64-1)
+        reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, d.d_result);
+        BM_HIP(hipGetLastError());
+    }
+
+    // 3. combine: one RCCL allgather of the 16-byte partials, or plain copies
+    int nslots = ndev;
+    if (ctx->world > 1) {
+        // one device per rank: gather every rank's partial over the process group
+        DeviceCtx& d = ctx->devs[0];
+        if (ncclAllGather(d.d_result, d.d_gather, 2, ncclUint64, d.comm, d.stream) != ncclSuccess) return BM_ERCCL;
+        BM_HIP(hipMemcpyAsync(d.h_result, d.d_gather, sizeof(Partial) * ctx->world, hipMemcpyDeviceToHost, d.stream));
+        nslots = ctx->world;
+    } else {
+        const bool use_rccl = ctx->combine == BM_COMBINE_RCCL ||
+                              (ctx->combine == BM_COMBINE_AUTO && ndev > 1 && distinct_devices(ctx));
+        if (use_rccl) {
+            int rc = ensure_nccl(ctx);
+            if (rc != BM_OK) return rc;
+            if (ncclGroupStart() != ncclSuccess) return BM_ERCCL;
+            for (int di = 0; di < ndev; ++di) {
+                DeviceCtx& d = ctx->devs[di];
+                if (ncclAllGather(d.d_result, d.d_gather, 2, ncclUint64, d.comm, d.stream) != ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    return BM_ERCCL;
+                }
+            }
+            if (ncclGroupEnd() != ncclSuccess) return BM_ERCCL;
+            DeviceCtx& d0 = ctx->devs[0];
+            BM_HIP(hipSetDevice(d0.id));
+            BM_HIP(hipMemcpyAsync(d0.h_result, d0.d_gather, sizeof(Partial) * ndev, hipMemcpyDeviceToHost,
+                                  d0.stream));
+        } else {
+            for (int di = 0; di < ndev; ++di) {
+                DeviceCtx& d = ctx->devs[di];
+                BM_HIP(hipSetDevice(d.id));
+                BM_HIP(hipMemcpyAsync(ctx->devs[0].h_result + di, d.d_result, sizeof(Partial),
+                                      hipMemcpyDeviceToHost, d.stream));
+            }
+        }
+    }
+    for (int di = 0; di < ndev; ++di) {
+        BM_HIP(hipSetDevice(ctx->devs[di].id));
+        BM_HIP(hipStreamSynchronize(ctx->devs[di].stream));
+    }
+
+    Partial best{UINT64_MAX, UINT64_MAX};
+    for (int i = 0; i < nslots; ++i) {
+        const Partial& p = ctx->devs[0].h_result[i];
+        if (p.hash < best.hash || (p.hash == best.hash && p.nonce < best.nonce)) best = p;
+    }
+    *best_out = best;
     return BM_OK;
 }
 
@@ -269,10 +400,23 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         out->nonce = UINT64_MAX;
         return BM_OK;
     }
-    st.nonces = upper - lower + 1;  // wraps to 0 only for the full 2^64 range
 
-    // 1. split the range over devices, plan and size every launch
-    const std::vector<Piece> pieces = split_range(lower, upper, ndev);
+    // 1. this process's piece (rank contexts: every rank passes the same
+    // range and scans its contiguous share of it), split over the devices;
+    // plan and size every launch
+    uint64_t lo = lower, hi = upper;
+    bool have = true;
+    if (ctx->world > 1) {
+        const std::vector<Piece> rp = split_range(lower, upper, ctx->world);
+        if (ctx->rank < (int)rp.size()) {
+            lo = rp[ctx->rank].lo;
+            hi = rp[ctx->rank].hi;
+        } else {
+            have = false;  // a range shorter than the group: nothing here
+        }
+    }
+    if (have) st.nonces = hi - lo + 1;  // wraps to 0 only for the full 2^64 range
+    const std::vector<Piece> pieces = have ? split_range(lo, hi, ndev) : std::vector<Piece>();
     std::vector<std::vector<Launch>> launches(ndev);
     for (int di = 0; di < ndev; ++di) {
         if (di >= (int)pieces.size()) continue;
@@ -288,7 +432,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
             for (size_t i = 1; i < segs.size(); ++i)
                 if (segs[i].vhi - segs[i].vlo > segs[big].vhi - segs[big].vlo) big = i;
             bm_segment_t& b = segs[big];
-            if (b.vhi - b.vlo >= 8 * ctx->tail_nonces) {
+            if ((b.vhi - b.vlo) / 8 >= ctx->tail_nonces) {
                 bm_segment_t t = b;
                 t.vlo = b.vhi - ctx->tail_nonces + 1;
                 b.vhi = t.vlo - 1;
@@ -311,84 +455,22 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         if (rc != BM_OK) return rc;
     }
 
-    // 2. enqueue: search launches, then the second-pass reduction
-    for (int di = 0; di < ndev; ++di) {
-        DeviceCtx& d = ctx->devs[di];
-        BM_HIP(hipSetDevice(d.id));
-        uint32_t nparts = 0, li = 0;
-        if (!launches[di].empty())
-            BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches[di].size() * sizeof(unsigned long long), d.stream));
-        // stream of each launch: biggest first, round-robin over the streams
-        const int ns = std::max(1, std::min<int>(ctx->streams, (int)launches[di].size()));
-        std::vector<uint32_t> order(launches[di].size());
-        for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
-        if (ns > 1) {
-            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-                return launches[di][a].stat.nonces > launches[di][b].stat.nonces;
-            });
-            BM_HIP(hipEventRecord(d.fork, d.stream));
-            for (int k = 0; k + 1 < ns; ++k) BM_HIP(hipStreamWaitEvent(d.aux[k], d.fork, 0));
-        }
-        for (uint32_t r = 0; r < order.size(); ++r) {
-            li = order[r];
-            Launch& L = launches[di][li];
-            hipStream_t s = (r % ns) == 0 ? d.stream : d.aux[r % ns - 1];
-            const bool timed = ctx->timing && li < (uint32_t)kEventPairs;
-            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li], s));
-            unsigned long long* ctr = d.d_ctr + li;
-            void* kargs[] = {&L.args, &d.d_part, &ctr};
-            BM_HIP(hipLaunchKernel(L.fn, dim3(L.grid), dim3(kBlock), kargs, 0, s));
-            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li + 1], s));
-            nparts += L.grid;
-        }
-        for (int k = 0; k + 1 < ns; ++k) {
-            BM_HIP(hipEventRecord(d.join[k], d.aux[k]));
-            BM_HIP(hipStreamWaitEvent(d.stream, d.join[k], 0));
-        }
-        reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, d.d_result);
-        BM_HIP(hipGetLastError());
-    }
-
-    // 3. combine: one RCCL allgather of the 16-byte partials, or plain copies
-    const bool use_rccl = ctx->combine == BM_COMBINE_RCCL || (ctx->combine == BM_COMBINE_AUTO && ndev > 1);
-    if (use_rccl) {
-        int rc = ensure_nccl(ctx);
-        if (rc != BM_OK) return rc;
-        if (ncclGroupStart() != ncclSuccess) return BM_ERCCL;
-        for (int di = 0; di < ndev; ++di) {
-            DeviceCtx& d = ctx->devs[di];
-            if (ncclAllGather(d.d_result, d.d_gather, 2, ncclUint64, d.comm, d.stream) != ncclSuccess) {
-                (void)ncclGroupEnd();
-                return BM_ERCCL;
-            }
-        }
-        if (ncclGroupEnd() != ncclSuccess) return BM_ERCCL;
-        DeviceCtx& d0 = ctx->devs[0];
-        BM_HIP(hipSetDevice(d0.id));
-        BM_HIP(hipMemcpyAsync(d0.h_result, d0.d_gather, sizeof(Partial) * ndev, hipMemcpyDeviceToHost, d0.stream));
-    } else {
-        for (int di = 0; di < ndev; ++di) {
-            DeviceCtx& d = ctx->devs[di];
-            BM_HIP(hipSetDevice(d.id));
-            BM_HIP(hipMemcpyAsync(ctx->devs[0].h_result + di, d.d_result, sizeof(Partial), hipMemcpyDeviceToHost,
-                                  d.stream));
-        }
-    }
-    for (int di = 0; di < ndev; ++di) {
-        BM_HIP(hipSetDevice(ctx->devs[di].id));
-        BM_HIP(hipStreamSynchronize(ctx->devs[di].stream));
-    }
-
-    Partial best{UINT64_MAX, UINT64_MAX};
-    for (int di = 0; di < ndev; ++di) {
-        const Partial& p = ctx->devs[0].h_result[di];
-        if (p.hash < best.hash || (p.hash == best.hash && p.nonce < best.nonce)) best = p;
+    // 2-3. enqueue, reduce, combine; a failure part-way drains every stream
+    // first, so the context stays usable
+    std::vector<uint32_t> first(ndev, 0);
+    Partial best;
+    const int rc = enqueue_and_combine(ctx, launches, first, &best);
+    if (rc != BM_OK) {
+        drain(ctx);
+        std::memset(&st, 0, sizeof st);
+        return rc;
     }
 
     // 4. statistics
     for (int di = 0; di < ndev; ++di) {
         DeviceCtx& d = ctx->devs[di];
         uint32_t li = 0;
+        const bool span_ok = ctx->timing && !launches[di].empty() && first[di] < (uint32_t)kEventPairs;
         for (Launch& L : launches[di]) {
             ++st.launches;
             if (ctx->timing && li < (uint32_t)kEventPairs) {
@@ -396,6 +478,11 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
                 BM_HIP(hipEventElapsedTime(&ms, d.ev[2 * li], d.ev[2 * li + 1]));
                 L.stat.ms = ms;
                 st.kernel_ms += ms;
+                if (span_ok) {  // the first launch's start to this launch's end
+                    float sp = 0.f;
+                    BM_HIP(hipEventElapsedTime(&sp, d.ev[2 * first[di]], d.ev[2 * li + 1]));
+                    st.span_ms = std::max(st.span_ms, (double)sp);
+                }
             }
             if (st.recorded < BM_MAX_LAUNCH_STATS) st.launch[st.recorded++] = L.stat;
             ++li;
@@ -404,6 +491,39 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     out->hash = best.hash;
     out->nonce = best.nonce;
+    return BM_OK;
+}
+
+// bm_reduce_gpu: n partials, one per lane, through block_min (ds_swizzle
+// butterflies, readlane, LDS) and then reduce_partials -- the reductions the
+// search uses above its per-lane scans.
+int reduce_impl(bm_ctx* ctx, const bm_result_t* in, size_t n, bm_result_t* out) {
+    DeviceCtx& d = ctx->devs[0];
+    BM_HIP(hipSetDevice(d.id));
+    const size_t blocks = (n + kBlock - 1) / kBlock;
+    const size_t need = n + blocks + 1;
+    if (need > d.test_cap) {
+        if (d.d_test) BM_HIP(hipFree(d.d_test));
+        d.d_test = nullptr;
+        d.test_cap = 0;
+        BM_HIP(hipMalloc(&d.d_test, need * sizeof(Partial)));
+        d.test_cap = need;
+    }
+    Partial* d_in = d.d_test;
+    Partial* d_blk = d.d_test + n;
+    Partial* d_out = d_blk + blocks;
+    if (n) BM_HIP(hipMemcpyAsync(d_in, in, n * sizeof(Partial), hipMemcpyHostToDevice, d.stream));
+    if (blocks) {
+        lane_partials_min<<<dim3((uint32_t)blocks), kBlock, 0, d.stream>>>(d_in, (uint32_t)n, d_blk);
+        BM_HIP(hipGetLastError());
+    }
+    reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d_blk, (uint32_t)blocks, d_out);
+    BM_HIP(hipGetLastError());
+    Partial r;
+    BM_HIP(hipMemcpyAsync(&r, d_out, sizeof r, hipMemcpyDeviceToHost, d.stream));
+    BM_HIP(hipStreamSynchronize(d.stream));
+    out->hash = r.hash;
+    out->nonce = r.nonce;
     return BM_OK;
 }
 
@@ -480,8 +600,26 @@ int bm_device_count(int* out) {
     return BM_OK;
 }
 
-int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out) {
-    if (!out || !devices || n < 1) return BM_EINVAL;
+}  // extern "C"
+
+namespace bm {
+namespace {
+// Environment knobs read at context creation.  Malformed or out-of-range
+// values keep the default (results never depend on them).
+void read_env(bm_ctx* ctx) {
+    if (const char* e = std::getenv("BTCMINER_STREAMS")) {
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= kMaxStreams) ctx->streams = v;
+    }
+    if (const char* e = std::getenv("BTCMINER_TAIL")) {
+        char* end = nullptr;
+        errno = 0;
+        const unsigned long long v = std::strtoull(e, &end, 10);
+        if (end != e && *end == '\0' && errno == 0 && v <= kMaxTailNonces) ctx->tail_nonces = v;
+    }
+}
+
+int create_ctx(const int* devices, int n, int nslots, bm_ctx** out) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count < 1) return BM_ENODEV;
     for (int i = 0; i < n; ++i)
@@ -489,22 +627,68 @@ int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out) {
     bm_ctx* ctx = new (std::nothrow) bm_ctx();
     if (!ctx) return BM_ENOMEM;
     std::memset(&ctx->stats, 0, sizeof ctx->stats);
-    if (const char* e = std::getenv("BTCMINER_STREAMS")) {
-        const int v = std::atoi(e);
-        if (v >= 1 && v <= bm::kMaxStreams) ctx->streams = v;
-    }
-    if (const char* e = std::getenv("BTCMINER_TAIL")) ctx->tail_nonces = std::strtoull(e, nullptr, 10);
-    bm::DeviceGuard guard;
+    read_env(ctx);
+    DeviceGuard guard;
     ctx->devs.resize(n);
     for (int i = 0; i < n; ++i) {
-        int rc = bm::init_device(ctx->devs[i], devices[i], n);
+        int rc = init_device(ctx->devs[i], devices[i], nslots);
         if (rc != BM_OK) {
-            for (auto& d : ctx->devs) bm::destroy_device(d);
+            for (auto& d : ctx->devs) destroy_device(d);
             delete ctx;
             return rc;
         }
     }
     *out = ctx;
+    return BM_OK;
+}
+}  // namespace
+}  // namespace bm
+
+extern "C" {
+
+int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out) {
+    if (!out || !devices || n < 1) return BM_EINVAL;
+    return bm::create_ctx(devices, n, n, out);
+}
+
+int bm_rccl_unique_id(uint8_t* id) {
+    if (!id) return BM_EINVAL;
+    static_assert(sizeof(ncclUniqueId) == BM_RCCL_ID_BYTES, "RCCL unique id size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return BM_ERCCL;
+    std::memcpy(id, &u, sizeof u);
+    return BM_OK;
+}
+
+int bm_ctx_create_rank(int device, int rank, int world, const uint8_t* id, bm_ctx_t** out) {
+    if (!out || !id || world < 1 || rank < 0 || rank >= world) return BM_EINVAL;
+    bm_ctx* ctx = nullptr;
+    int rc = bm::create_ctx(&device, 1, world, &ctx);
+    if (rc != BM_OK) return rc;
+    ctx->rank = rank;
+    ctx->world = world;
+    bm::DeviceGuard guard;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    if (hipSetDevice(device) != hipSuccess) {
+        bm_ctx_destroy(ctx);
+        return BM_EHIP;
+    }
+    // blocks until every rank of the group has called it
+    if (ncclCommInitRank(&ctx->devs[0].comm, world, u, rank) != ncclSuccess) {
+        ctx->devs[0].comm = nullptr;
+        bm_ctx_destroy(ctx);
+        return BM_ERCCL;
+    }
+    ctx->nccl_ready = true;
+    *out = ctx;
+    return BM_OK;
+}
+
+int bm_ctx_rank(const bm_ctx_t* ctx, int* rank, int* world) {
+    if (!ctx || !rank || !world) return BM_EINVAL;
+    *rank = ctx->rank;
+    *world = ctx->world;
     return BM_OK;
 }
 
@@ -542,6 +726,21 @@ int bm_search_gpu(bm_ctx_t* ctx, const uint8_t* msg, size_t len, uint64_t lower,
     return rc;
 }
 
+int bm_reduce_gpu(bm_ctx_t* ctx, const bm_result_t* parts, size_t n, bm_result_t* out) {
+    if (!ctx || !out || (n && !parts) || n > BM_MAX_REDUCE) return BM_EINVAL;
+    bm::DeviceGuard guard;
+    bm_result_t r;
+    int rc = bm::reduce_impl(ctx, parts, n, &r);
+    if (rc == BM_OK) *out = r;
+    return rc;
+}
+
+int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches) {
+    if (!ctx || launches < -1) return BM_EINVAL;
+    ctx->fault_after = launches;
+    return BM_OK;
+}
+
 int bm_hash_gpu(bm_ctx_t* ctx, const uint8_t* msg, size_t len, const uint64_t* nonces, size_t n, uint64_t* out) {
     if (!ctx || (n && (!nonces || !out)) || (len && !msg) || len > BM_MAX_MSG_LEN) return BM_EINVAL;
     bm::DeviceGuard guard;
@@ -568,6 +767,7 @@ int bm_ctx_set_blocks_per_cu(bm_ctx_t* ctx, int blocks_per_cu) {
 
 int bm_ctx_set_combine(bm_ctx_t* ctx, int mode) {
     if (!ctx || mode < BM_COMBINE_AUTO || mode > BM_COMBINE_HOST) return BM_EINVAL;
+    if (ctx->world > 1 && mode == BM_COMBINE_HOST) return BM_EINVAL;  // ranks combine over RCCL
     ctx->combine = mode;
     return BM_OK;
 }

@@ -1,6 +1,8 @@
 // bm_aux_kernels.hpp -- the small kernels around the search kernel:
 //   reduce_partials : second pass, lexicographic min of the per-workgroup
 //                     partials of one search on one device -> 16 bytes.
+//   lane_partials_min : the search kernel's workgroup reduction over given
+//                     partials (bm_reduce_gpu, a test entry for the tie rule).
 //   hash_kernel     : batched bitcoin.Hash (hash.go:11-15) for arbitrary
 //                     nonces, used by bm_hash_gpu (parity tests, the Hash
 //                     mirror).  Not on the search hot path.
@@ -22,6 +24,20 @@ __global__ __launch_bounds__(kReduceThreads) void reduce_partials(const Partial*
         }
     }
     if (block_min<kReduceThreads>(h, nn)) *out = Partial{h, nn};
+}
+
+// Test entry of the reductions (bm_reduce_gpu): one partial per lane
+// (beyond n: the empty (2^64-1, 2^64-1)), the search kernel's block_min
+// (ds_swizzle butterflies, readlane, LDS), one partial per workgroup.
+__global__ __launch_bounds__(kBlock) void lane_partials_min(const Partial* __restrict__ in, uint32_t n,
+                                                            Partial* __restrict__ out) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    uint64_t h = ~0ull, nn = ~0ull;
+    if (i < n) {
+        h = in[i].hash;
+        nn = in[i].nonce;
+    }
+    if (block_min<kBlock>(h, nn)) out[blockIdx.x] = Partial{h, nn};
 }
 
 constexpr int kHashThreads = 64;

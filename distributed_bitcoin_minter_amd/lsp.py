@@ -85,10 +85,29 @@ class Message:
 
     @classmethod
     def unmarshal(cls, raw):
-        d = json.loads(raw)
+        """json.Unmarshal into a Message.  Anything that is not an object with
+        integer Type/ConnID/SeqNum and a base64 (or null) Payload raises
+        ValueError, so a stray datagram can never stop an endpoint's reader."""
+        try:
+            d = json.loads(raw)
+        except (UnicodeDecodeError, RecursionError) as e:
+            raise ValueError(f"not a JSON message: {e!r}") from None
+        if not isinstance(d, dict):
+            raise ValueError("LSP message is not a JSON object")
+        vals = []
+        for f in ("Type", "ConnID", "SeqNum"):
+            v = d.get(f)
+            if v is None:
+                v = 0
+            if isinstance(v, bool) or not isinstance(v, int) or not -(1 << 63) <= v < 1 << 63:
+                raise ValueError(f"LSP field {f} is not an int")
+            vals.append(v)
         p = d.get("Payload")
-        return cls(int(d.get("Type", 0)), int(d.get("ConnID", 0)), int(d.get("SeqNum", 0)),
-                   None if p is None else base64.b64decode(p))
+        if p is not None:
+            if not isinstance(p, str):
+                raise ValueError("LSP Payload is not a base64 string")
+            p = base64.b64decode(p, validate=True)  # binascii.Error is a ValueError
+        return cls(vals[0], vals[1], vals[2], p)
 
     def String(self):
         name = {MsgConnect: "Connect", MsgData: "Data", MsgAck: "Ack"}.get(self.Type, "")

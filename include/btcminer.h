@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BM_ABI_VERSION 1
+#define BM_ABI_VERSION 2
 
 /* status codes */
 #define BM_OK 0
@@ -77,8 +77,24 @@ int bm_device_count(int* out);
  * short-task launch of their own (default 16777216, 0 = off). */
 int bm_ctx_create(int num_gpus, bm_ctx_t** out);
 /* Context over an explicit device list (e.g. {LOCAL_RANK} for one process
- * per GPU). */
+ * per GPU).  A device listed twice is allowed (a one-GPU rehearsal of the
+ * N-device split); such a context combines on the host. */
 int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out);
+
+/* ---- one process per GPU: a context that is one rank of an RCCL group ----
+ * Rank 0 calls bm_rccl_unique_id() and hands the bytes to every rank
+ * (any side channel: torch.distributed's store, a file, MPI...); each rank
+ * then calls bm_ctx_create_rank() on its own device, which blocks until the
+ * whole group has joined (ncclCommInitRank).  After that every rank calls
+ * bm_search_gpu() with the SAME (msg, lower, upper): rank r scans the r-th
+ * of `world` contiguous near-equal pieces of the range, and one RCCL
+ * allgather of the 16-byte partials gives every rank the result for the
+ * whole range.  The reference's equivalent is the server handing each miner
+ * a piece of the request (bitcoin/server/server.go:153-169). */
+#define BM_RCCL_ID_BYTES 128
+int bm_rccl_unique_id(uint8_t* id /* BM_RCCL_ID_BYTES */);
+int bm_ctx_create_rank(int device, int rank, int world, const uint8_t* id, bm_ctx_t** out);
+int bm_ctx_rank(const bm_ctx_t* ctx, int* rank, int* world);
 int bm_ctx_destroy(bm_ctx_t* ctx);
 int bm_ctx_num_devices(const bm_ctx_t* ctx, int* out);
 
@@ -113,7 +129,10 @@ typedef struct bm_stats {
     uint32_t launches;     /* search-kernel launches of the last call */
     uint32_t recorded;     /* entries filled in launch[] (<= BM_MAX_LAUNCH_STATS) */
     double wall_ms;        /* host wall time of the last bm_search_gpu call */
-    double kernel_ms;      /* sum of launch durations (timing on) */
+    double kernel_ms;      /* SUM of launch durations (timing on); launches on
+                              different streams overlap, so this can exceed span_ms */
+    double span_ms;        /* first launch's start to the last launch's end on
+                              one device (timing on; max over devices) */
     uint64_t nonces;       /* nonces in the last call */
     bm_launch_stat_t launch[BM_MAX_LAUNCH_STATS];
 } bm_stats_t;
@@ -149,6 +168,21 @@ int bm_ctx_set_task_digits(bm_ctx_t* ctx, int digits);
 #define BM_COMBINE_RCCL 1
 #define BM_COMBINE_HOST 2
 int bm_ctx_set_combine(bm_ctx_t* ctx, int mode);
+
+/* ---- test entries (do not change search results) ---------------------- */
+
+/* Lexicographic (hash, nonce) min of n partials on the first device of ctx,
+ * computed by the reductions the search runs above its per-lane scans
+ * (ds_swizzle/readlane wave min, LDS workgroup min, second-pass kernel).
+ * Pins the tie rule (equal hashes -> smallest nonce, miner.go:61) on inputs
+ * the search itself cannot produce.  n <= BM_MAX_REDUCE. */
+#define BM_MAX_REDUCE (1u << 24)
+int bm_reduce_gpu(bm_ctx_t* ctx, const bm_result_t* parts, size_t n, bm_result_t* out);
+
+/* Make every later bm_search_gpu fail with BM_EINTERNAL after enqueueing
+ * `launches` search launches (-1: off).  Exercises the failure path: the
+ * call drains what it queued and the context stays usable. */
+int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches);
 
 /* ---- host-side plan introspection (pure CPU; used by the CPU tests) ---- */
 

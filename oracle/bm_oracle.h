@@ -59,6 +59,14 @@ int oracle_search_mt(const uint8_t* msg, size_t len, uint64_t lower, uint64_t up
                      int nthreads, int use_openssl,
                      uint64_t* out_hash, uint64_t* out_nonce);
 
+/* The same inclusive search with 16 lanes of AVX-512 per thread
+ * (bm_scan16.c): midstate, digits stepped in place, 16 compressions at a
+ * time.  Only for golden answers over ranges of 2^32..2^40 nonces; checked
+ * against oracle_search() by tests/test_oracle.py.  Returns 0, or -2 when the
+ * CPU lacks AVX-512F. */
+int oracle_search_x16(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, int nthreads,
+                      uint64_t* out_hash, uint64_t* out_nonce);
+
 /* Hash a list of nonces (scalar restatement). */
 void oracle_hash_many(const uint8_t* msg, size_t len, const uint64_t* nonces, size_t n,
                       uint64_t* out);

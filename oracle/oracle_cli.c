@@ -2,6 +2,7 @@
  * oracle_cli -- command-line front end of the CPU oracle (test infra only).
  *   oracle_cli hash   <msg-hex> <nonce>
  *   oracle_cli search <msg-hex> <lower> <upper> [threads] [openssl:0|1]
+ *   oracle_cli search16 <msg-hex> <lower> <upper> [threads]   (AVX-512, bm_scan16.c)
  * Prints "<hash> <nonce>" (decimal), the same pair the reference client
  * prints as "Result <hash> <nonce>" (bitcoin/client/client.go:76-78).
  */
@@ -39,6 +40,13 @@ int main(int argc, char** argv) {
         uint64_t lo = strtoull(argv[3], NULL, 10), hi = strtoull(argv[4], NULL, 10), h, n;
         int th = argc > 5 ? atoi(argv[5]) : 1, ossl = argc > 6 ? atoi(argv[6]) : 0;
         if (oracle_search_mt(msg, len, lo, hi, th, ossl, &h, &n)) return 1;
+        printf("%llu %llu\n", (unsigned long long)h, (unsigned long long)n);
+        return 0;
+    }
+    if (!strcmp(argv[1], "search16") && argc >= 5) {
+        uint64_t lo = strtoull(argv[3], NULL, 10), hi = strtoull(argv[4], NULL, 10), h, n;
+        int th = argc > 5 ? atoi(argv[5]) : 1;
+        if (oracle_search_x16(msg, len, lo, hi, th, &h, &n)) return 1;
         printf("%llu %llu\n", (unsigned long long)h, (unsigned long long)n);
         return 0;
     }

@@ -16,9 +16,9 @@ U64 = (1 << 64) - 1
 
 
 def pytest_configure(config):
-    # libbtcminer.so binds to whichever libamdhip64 is loaded first; torch
-    # bundles its own.  Keep torch out of this process so the GPU tests run
-    # on /opt/rocm's runtime (bench.py imports torch first, on purpose).
+    # libbtcminer.so binds to /opt/rocm's HIP runtime; torch bundles its own.
+    # Keep torch out of this process so only one runtime is mapped (bench.py
+    # does the same: torch.distributed runs in a rendezvous sidecar process).
     config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) GPU")
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
@@ -41,6 +41,8 @@ class Oracle:
         lib.oracle_search_mt.argtypes = [ctypes.c_char_p, ctypes.c_size_t, u64, u64, ctypes.c_int, ctypes.c_int,
                                          P(u64), P(u64)]
         lib.oracle_search_mt.restype = ctypes.c_int
+        lib.oracle_search_x16.argtypes = [ctypes.c_char_p, ctypes.c_size_t, u64, u64, ctypes.c_int, P(u64), P(u64)]
+        lib.oracle_search_x16.restype = ctypes.c_int
         self.lib = lib
 
     def hash(self, msg: bytes, nonce: int) -> int:
@@ -53,6 +55,16 @@ class Oracle:
         else:
             assert self.lib.oracle_search_mt(msg, len(msg), lo, hi, threads, 1 if openssl else 0,
                                              ctypes.byref(h), ctypes.byref(n)) == 0
+        return h.value, n.value
+
+    def search_x16(self, msg: bytes, lo: int, hi: int, threads: int = 8):
+        """16-lane AVX-512 scan (oracle/bm_scan16.c): golden answers over long
+        ranges only, itself checked against search() (tests/test_oracle.py)."""
+        h, n = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self.lib.oracle_search_x16(msg, len(msg), lo, hi, threads, ctypes.byref(h), ctypes.byref(n))
+        if rc == -2:
+            raise OSError("oracle_search_x16 needs AVX-512F")
+        assert rc == 0
         return h.value, n.value
 
     def search_excl(self, msg: bytes, lo: int, hi: int):

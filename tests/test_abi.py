@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     lib = _lib.load()
-    assert lib.bm_abi_version() == 1
+    assert lib.bm_abi_version() == _lib.BM_ABI_VERSION == 2
     for code in range(0, -7, -1):
         assert lib.bm_strerror(code).decode() != "unknown status"
     assert lib.bm_strerror(-99).decode() == "unknown status"
@@ -46,6 +46,15 @@ def test_invalid_arguments_rejected():
     assert lib.bm_ctx_destroy(None) == _lib.BM_EINVAL
     n = ctypes.c_int()
     assert lib.bm_plan_segments(b"x", 1, 0, 1, None, 1, ctypes.byref(n)) == _lib.BM_EINVAL
+    h = ctypes.c_void_p()
+    uid = b"\0" * _lib.BM_RCCL_ID_BYTES
+    assert lib.bm_rccl_unique_id(None) == _lib.BM_EINVAL
+    for dev, rank, world in [(0, 0, 0), (0, 2, 2), (0, -1, 2)]:
+        assert lib.bm_ctx_create_rank(dev, rank, world, uid, ctypes.byref(h)) == _lib.BM_EINVAL
+    assert lib.bm_ctx_create_rank(0, 0, 1, None, ctypes.byref(h)) == _lib.BM_EINVAL
+    assert lib.bm_reduce_gpu(None, None, 0, ctypes.byref(r)) == _lib.BM_EINVAL
+    assert lib.bm_ctx_set_test_fault(None, 0) == _lib.BM_EINVAL
+    assert lib.bm_ctx_rank(None, ctypes.byref(n), ctypes.byref(n)) == _lib.BM_EINVAL
 
 
 @pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")
@@ -53,6 +62,17 @@ def test_no_gpu_fails_loudly():
     with pytest.raises(_lib.BtcMinerError) as ei:
         _lib.Context(num_gpus=1)
     assert ei.value.status == _lib.BM_ENODEV
+    with pytest.raises(_lib.BtcMinerError) as ei:
+        _lib.Context(devices=[0], rank=0, world=1, unique_id=b"\0" * _lib.BM_RCCL_ID_BYTES)
+    assert ei.value.status == _lib.BM_ENODEV
+
+
+def test_library_loads_with_immediate_binding():
+    """_lib loads libbtcminer.so with RTLD_NOW: its HIP/RCCL symbols bind to
+    /opt/rocm's runtime at load, before any later `import torch` maps torch's
+    bundled copy (bench.py's torchrun path)."""
+    import inspect
+    assert "RTLD_NOW" in inspect.getsource(_lib.load)
 
 
 def _c_client():
@@ -60,7 +80,8 @@ def _c_client():
     (built by __graft_entry__.build(); rebuilt here if absent)."""
     import subprocess
     exe = os.path.join(ROOT, "examples", "bm_c_client")
-    if not os.path.exists(exe):
+    deps = [os.path.join(ROOT, "examples", "bm_c_client.c"), os.path.join(ROOT, "include", "btcminer.h")]
+    if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(d) for d in deps):
         subprocess.check_call(["gcc", "-O2", "-I", os.path.join(ROOT, "include"),
                                os.path.join(ROOT, "examples", "bm_c_client.c"),
                                "-L", os.path.join(ROOT, "distributed_bitcoin_minter_amd"), "-lbtcminer",

@@ -1,14 +1,18 @@
-"""Multi-rank sharding (distributed_bitcoin_minter_amd/dist.py) on CPU with
-gloo, world_size 2 and 4: each rank scans its piece (with the CPU oracle
-standing in for the per-rank GPU search), one all_gather of 16-byte
-partials, lexicographic min == the single-process scan.
+"""Multi-rank sharding on CPU: the range split (dist.split_range, the mirror of
+bm::split_range), the lexicographic combine, and the torchrun-style
+rendezvous (distributed_bitcoin_minter_amd/rendezvous.py: torch.distributed
+gloo in a sidecar process) at world sizes 2 and 4.  On CPU each rank's scan
+is the oracle; the same workers run the HIP search in the -m gpu variant
+(every rank on GPU 0), so no N>1 test is left without the real kernels.
 
-torch is imported only inside the spawned workers: the pytest process
-keeps a single HIP runtime (/opt/rocm's) for the GPU tests."""
-import multiprocessing as mp
+torch is imported only inside the sidecars: the pytest process keeps a
+single HIP runtime (/opt/rocm's) for the GPU tests."""
+import json
 import os
 import random
 import socket
+import subprocess
+import sys
 
 import pytest
 
@@ -29,6 +33,13 @@ def test_split_range_tiles_exactly():
         assert max(sizes) - min(sizes) <= 1
 
 
+def test_split_range_weak_scaling_pieces():
+    """bench.py's weak-scaling ranges [0, N*2^32-1] split into exactly the
+    per-GPU pieces [r*2^32, (r+1)*2^32-1] the goldens are keyed on."""
+    for n in (1, 2, 4, 8):
+        assert split_range(0, n * 2 ** 32 - 1, n) == [(r * 2 ** 32, (r + 1) * 2 ** 32 - 1) for r in range(n)]
+
+
 def test_lex_min_tie_goes_to_smallest_nonce():
     assert lex_min([(5, 9), (5, 3), (7, 1)]) == (5, 3)
     assert lex_min([]) == (U64, U64)
@@ -42,35 +53,75 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, msg, lo, hi, q):
-    import sys
-    sys.path.insert(0, ROOT)
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import torch.distributed as dist
+# One rank: rendezvous (gloo sidecar), a broadcast of rank 0's bytes (the
+# RCCL unique id's path), its piece scanned (oracle on CPU, HIP on GPU),
+# gather + lexicographic min, max over ranks.
+_RANK = r"""
+import json, os, sys
+root, mode, msg_hex, lo, hi = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+sys.path[:0] = [root, os.path.join(root, "tests")]
+from distributed_bitcoin_minter_amd.dist import lex_min, rank_piece
+from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
+msg = bytes.fromhex(msg_hex)
+if mode == "gpu":
+    from distributed_bitcoin_minter_amd import Context
+    ctx = Context(devices=[0])
+    scan = ctx.search
+else:
     from conftest import Oracle
-    from distributed_bitcoin_minter_amd.dist import combine
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    oracle = Oracle(os.path.join(ROOT, "oracle", "liboracle.so"))
-    piece = rank_piece(lo, hi, rank, world)
-    part = oracle.search(msg, *piece) if piece else (U64, U64)
-    res = combine(part)
-    q.put((rank, res))
-    dist.destroy_process_group()
+    scan = Oracle(os.path.join(root, "oracle", "liboracle.so")).search
+with Rendezvous(timeout_s=120) as rz:
+    token = rz.broadcast_bytes(os.urandom(128) if rz.rank == 0 else None)
+    piece = rank_piece(lo, hi, rz.rank, rz.world)
+    part = scan(msg, *piece) if piece else (2**64 - 1, 2**64 - 1)
+    res = lex_min(tuple(p) for p in rz.all_gather(list(part)))
+    mx = rz.all_max(float(rz.rank))
+    rz.barrier()
+print(json.dumps({"rank": rz.rank, "token": token.hex(), "res": list(res), "max": mx, "piece": piece}))
+"""
+
+
+def _run_ranks(world, mode, msg, lo, hi):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE=str(world))
+        procs.append(subprocess.Popen([sys.executable, "-c", _RANK, ROOT, mode, msg.hex(), str(lo), str(hi)],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=300)
+        assert p.returncode == 0, e[-3000:]
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    return outs
+
+
+def _check(outs, world, want, lo, hi):
+    assert len({o["token"] for o in outs}) == 1  # rank 0's bytes reached every rank
+    assert all(o["max"] == world - 1 for o in outs)
+    assert all(tuple(o["res"]) == want for o in outs), outs
+    pieces = [tuple(o["piece"]) for o in sorted(outs, key=lambda o: o["rank"]) if o["piece"]]
+    assert pieces == split_range(lo, hi, world)
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_gloo_combine_equals_single_scan(oracle, world):
+def test_rendezvous_combine_equals_single_scan(oracle, world):
     msg, lo, hi = b"bradfitz", 0, 99_999
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, msg, lo, hi, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    out = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    expect = oracle.search(msg, lo, hi)
-    assert all(res == expect for _, res in out), out
+    _check(_run_ranks(world, "cpu", msg, lo, hi), world, oracle.search(msg, lo, hi), lo, hi)
+
+
+def test_rendezvous_range_shorter_than_world(oracle):
+    msg, lo, hi = b"msg", 1, 2  # 2 nonces over 4 ranks: ranks 2, 3 scan nothing
+    outs = _run_ranks(4, "cpu", msg, lo, hi)
+    assert [o["piece"] for o in sorted(outs, key=lambda o: o["rank"])] == [[1, 1], [2, 2], None, None]
+    assert all(tuple(o["res"]) == oracle.search(msg, lo, hi) for o in outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_rendezvous_ranks_on_gpu(oracle, world):
+    """The same ranks with the HIP search (every rank on GPU 0): a window
+    across the 9->10 digit boundary, split over the ranks."""
+    msg, lo, hi = b"bradfitz", 999_000_000, 1_000_999_999
+    _check(_run_ranks(world, "gpu", msg, lo, hi), world, oracle.search(msg, lo, hi, threads=8), lo, hi)

@@ -263,3 +263,40 @@ def test_server_fast_close_delivers_pending():
     lspnet.SetServerWriteDropPercent(0)
     assert [c.Read() for _ in range(10)] == [b"s%d" % i for i in range(10)]
     c.Close()
+
+
+GARBAGE = [b"null", b"[]", b'"x"', b"42", b"{", b"\xff", b'{"Type":1,"Payload":5}',
+           b'{"Type":"1","ConnID":1}', b'{"Type":1,"ConnID":1,"SeqNum":1,"Payload":"***"}',
+           b'{"Type":1,"ConnID":1.5}', b'{"Type":true}', b"[" * 100000]
+
+
+def test_lsp_message_unmarshal_rejects_garbage():
+    for raw in GARBAGE:
+        with pytest.raises(ValueError):
+            lsp.Message.unmarshal(raw)
+
+
+def test_garbage_datagrams_do_not_stop_endpoints():
+    """Stray datagrams (not JSON objects, wrong field types, bad base64) sent to
+    the server and to a client are dropped; both readers keep running and the
+    connection still echoes (one bad packet used to kill a reader
+    thread)."""
+    import socket
+    p = params(ms=30, k=20)
+    srv, stop, t = echo_server(p)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", p)
+    c.Write(b"before")
+    assert c.Read() == b"before"
+    caddr = c._conn._sock.getsockname() if hasattr(c._conn, "_sock") else None
+    with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+        for raw in GARBAGE:
+            s.sendto(raw[:1400], ("127.0.0.1", srv.port))
+            if caddr:
+                s.sendto(raw[:1400], caddr)
+    time.sleep(0.2)
+    for i in range(5):
+        c.Write(f"after-{i}".encode())
+        assert c.Read() == f"after-{i}".encode()
+    c.Close()
+    stop.set()
+    srv.Close()

@@ -42,6 +42,25 @@ def test_rejects_out_of_range():
         Message.unmarshal(b'{"Type":1,"Lower":18446744073709551616}')
 
 
+BAD_PAYLOADS = [b"null", b"[]", b'"x"', b"5", b"{", b"\xff\xfe", b'{"Type":null,"Data":5}',
+                b'{"Type":1,"Data":5}', b'{"Type":1,"Data":["a"]}', b'{"Type":1,"Lower":1.5}',
+                b'{"Type":1,"Lower":"7"}', b'{"Type":1,"Upper":true}', b'{"Type":2,"Hash":-1}',
+                b'{"Type":"1"}', b'{"Type":1.0}', b'{"Type":9}', b'{"Type":2,"Nonce":{}}']
+
+
+@pytest.mark.parametrize("raw", BAD_PAYLOADS)
+def test_unmarshal_rejects_malformed(raw):
+    """Payloads Go's json.Unmarshal would reject (or that are not a Message
+    at all) raise ValueError, the one error the server, miner and client
+    catch for a bad message."""
+    with pytest.raises(ValueError):
+        Message.unmarshal(raw)
+
+
+def test_unmarshal_null_fields_keep_zero_values():
+    assert Message.unmarshal(b'{"Type":1,"Data":null,"Lower":null,"Upper":9}') == NewRequest("", 0, 9)
+
+
 def test_invalid_utf8_becomes_replacement_char_like_go():
     """Go's encoding/json replaces invalid UTF-8 in a string with U+FFFD, so a
     Go miner hashes the replacement's bytes.  A Python str

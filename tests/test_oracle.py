@@ -5,6 +5,7 @@ answers, 1,000 hashlib Hash vectors, hashlib min-scan vectors at block and
 digit-count edges, and the whole-range answers of C1/C2/C3.
 """
 import os
+import random
 
 import pytest
 
@@ -59,3 +60,33 @@ def test_openssl_and_scalar_agree(oracle):
     msg = b"The quick brown fox"
     for lo, hi in [(0, 5000), (U64 - 5000, U64), (999_999_000, 1_000_001_000)]:
         assert oracle.search(msg, lo, hi, threads=4, openssl=True) == oracle.search(msg, lo, hi)
+
+
+def test_x16_scanner_agrees_with_oracle(oracle):
+    """The AVX-512 16-lane scan used for the long-range goldens (2^35 weak
+    scaling, 2^40 C4) equals the byte-string oracle on every message-length
+    class (1 and 2 final blocks, midstate of 0..9 whole blocks), across
+    10^k digit boundaries, at 2^64-1, on ranges shorter than 16 lanes and on
+    raw bytes."""
+    try:
+        oracle.search_x16(b"msg", 0, 2)
+    except OSError:
+        pytest.skip("no AVX-512F on this CPU")
+    assert oracle.search_x16(b"msg", 0, 2, threads=1) == (4754799531757243342, 1)  # README:331
+    assert oracle.search_x16(b"msg", 5, 4) == (U64, U64)
+    rng = random.Random(0x5EED)
+    lens = [0, 1, 7, 8, 44, 45, 46, 53, 54, 55, 56, 62, 63, 64, 65, 119, 120, 127, 128, 600]
+    for k in range(60):
+        L = lens[k % len(lens)] if k < 40 else rng.randint(0, 300)
+        msg = bytes(rng.randrange(256) for _ in range(L))
+        D = rng.randint(1, 20)
+        if k % 3 == 0:  # straddle 10^D
+            c = 10 ** D if D < 20 else U64 - 3000
+            lo, hi = max(0, c - rng.randint(1, 3000)), min(U64, c + rng.randint(0, 3000))
+        else:
+            lo = rng.randint(0 if D == 1 else 10 ** (D - 1), U64 if D == 20 else 10 ** D - 1)
+            hi = min(U64, lo + rng.choice([0, 1, 5, 15, 16, 17, 999, 5000]))
+        want = oracle.search(msg, lo, hi, threads=4)
+        assert oracle.search_x16(msg, lo, hi, threads=rng.choice([1, 3, 8])) == want, (L, lo, hi)
+    assert oracle.search_x16(b"bradfitz", U64 - 4000, U64) == oracle.search(b"bradfitz", U64 - 4000, U64)
+    assert oracle.search_x16(b"bradfitz", 0, 9999) == (1419516646206828, 9898)

@@ -451,3 +451,21 @@ def test_depth_two_queues_the_next_job():
             s._on_message(m, NewResult(lo + 1, lo))
     s._on_message(1, NewResult(99, 50))    # (50, 59) went to miner 1 when it freed up
     assert f.results_for(100) == [(5, 5)]
+
+
+def test_server_survives_malformed_client_payloads(oracle):
+    """A client whose LSP payloads are not valid bitcoin Messages (null, an
+    array, Data not a string, a float nonce ...) is logged and ignored; the
+    server keeps serving, including that client's later valid Request
+    (these used to crash the server loop)."""
+    s = System(chunk=1000, p=params())
+    s.add_miner(OracleSearcher(oracle))
+    c = lsp.NewClient(s.hostport, params())
+    for raw in [b"null", b"[]", b"7", b'{"Type":1,"Data":5,"Upper":10}', b'{"Type":1,"Data":"x","Upper":1.5}',
+                b'{"Type":1,"Data":["x"],"Upper":10}', b'{"Type":"1"}', b"\xff"]:
+        c.Write(raw)
+    c.Write(NewRequest("bradfitz", 0, 9999).marshal())
+    got = Message.unmarshal(c.Read())
+    assert (got.Type, got.Hash, got.Nonce) == (MsgType.Result, 1419516646206828, 9898)
+    c.Close()
+    s.close()
