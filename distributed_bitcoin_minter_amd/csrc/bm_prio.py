@@ -65,8 +65,22 @@ def _operands(rest):
     return [o.strip() for o in rest.split(" bitop3:")[0].split(",") if o.strip()]
 
 
+# VOP3B forms: vdst, sdst, src...  (the second operand is an SGPR the op writes)
+VOP3B_RE = re.compile(r"^v_(add|sub|subrev|addc|subb|subbrev)_co_|^v_(mad|mul)_[ui]64_|^v_div_scale")
+
+
+def _sreg_nums(tok):
+    if SREG_RE.match(tok):
+        return [int(SREG_RE.match(tok).group(1))]
+    r = SRANGE_RE.match(tok)
+    if r:
+        return list(range(int(r.group(1)), int(r.group(2)) + 1))
+    return []
+
+
 def _sdefs(line):
-    """SGPR numbers an instruction writes (its first operand), conservatively."""
+    """SGPR numbers an instruction writes: its first operand, and the carry /
+    scale SGPR destination of VOP3B forms (v_add_co_u32_e64 v, s[..], ...)."""
     m = re.match(r"^\s+([sv]_[a-z0-9_]+)\s*(.*)$", line)
     if not m or m.group(1).startswith(("s_cmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "s_setprio",
                                         "s_endpgm", "s_barrier", "s_sleep")):
@@ -74,13 +88,10 @@ def _sdefs(line):
     ops = _operands(m.group(2))
     if not ops:
         return []
-    d = ops[0]
-    if SREG_RE.match(d):
-        return [int(SREG_RE.match(d).group(1))]
-    r = SRANGE_RE.match(d)
-    if r:
-        return list(range(int(r.group(1)), int(r.group(2)) + 1))
-    return []
+    out = _sreg_nums(ops[0].split()[0])
+    if VOP3B_RE.match(m.group(1)) and len(ops) > 1:
+        out += _sreg_nums(ops[1].split()[0])
+    return out
 
 
 def fold_sgpr_constants(lines, kernels):

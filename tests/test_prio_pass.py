@@ -156,3 +156,32 @@ _ZN2bm13search_kernelILi18ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
         assert run_block(lines, regs) == run_block(out, regs)
     out2, n2 = bm_prio.split_add3(lines, ["search_kernel"], 2)
     assert n2 == 1
+
+
+def test_vop3b_carry_destination_counts_as_a_definition():
+    """An SGPR set by s_mov_b32 and ALSO written as the carry-out of a VOP3B op
+    (v_add_co_u32_e64 v, s[..], ...) holds that constant only until the carry
+    write: the pass must not fold it after that point, neither through the
+    whole-kernel 'single definition' rule nor the in-block rule."""
+    k = """\
+_ZN2bm13search_kernelILi18ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
+\ts_mov_b32 s20, 0x923f82a4
+\ts_mov_b32 s21, 0x11111111
+.LBB5_1:
+\tv_add_u32_e32 v1, s20, v2
+\tv_add_co_u32_e64 v3, s[20:21], v4, v5
+\tv_add_u32_e32 v6, s20, v7
+\tv_add3_u32 v8, s21, v9, v10
+\tv_mad_u64_u32 v[12:13], s[22:23], v14, v15, 0
+\ts_cbranch_scc1 .LBB5_1
+.Lfunc_end5:
+"""
+    assert bm_prio._sdefs("\tv_add_co_u32_e64 v3, s[20:21], v4, v5") == [20, 21]
+    assert bm_prio._sdefs("\tv_mad_u64_u32 v[12:13], s[22:23], v14, v15, 0") == [22, 23]
+    assert bm_prio._sdefs("\tv_add_u32_e32 v1, s20, v2") == []
+    out, n_fold, n_split = bm_prio.fold_sgpr_constants(k.splitlines(keepends=True), ["search_kernel"])
+    out = "".join(out)
+    assert n_fold == 0 and n_split == 0
+    # s20 / s21 have two definitions: no literal may replace them anywhere
+    assert "0x923f82a4, v2" not in out and "0x923f82a4, v7" not in out
+    assert "v_add_u32_e32 v6, s20, v7" in out and "v_add3_u32 v8, s21, v9, v10" in out
