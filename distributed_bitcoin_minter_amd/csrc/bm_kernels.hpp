@@ -119,6 +119,39 @@ BM_DEV uint32_t ssig0_uniform(uint32_t x) {
     return ((x >> 7) | (x << 25)) ^ ((x >> 18) | (x << 14)) ^ (x >> 3);
 }
 
+#ifndef BM_PIN  // SALU sigma0(J) + VGPR copies of launch constants in the inner loop (A/B knob)
+#define BM_PIN 1
+#endif
+
+// sigma0 of a wave-uniform word on the scalar unit.  Written in C, LLVM turns
+// the rotates into v_alignbit reading the SGPR (two slow VALU ops per nonce);
+// here they stay SALU (its own issue port), and only the final xor with the
+// per-lane part is a VALU op.
+BM_DEV uint32_t ssig0_salu(uint32_t x) {
+    uint32_t r, t0, t1, t2;
+    asm("s_lshr_b32 %1, %4, 7\n\t"
+        "s_lshl_b32 %2, %4, 25\n\t"
+        "s_or_b32 %1, %1, %2\n\t"
+        "s_lshr_b32 %2, %4, 18\n\t"
+        "s_lshl_b32 %3, %4, 14\n\t"
+        "s_or_b32 %2, %2, %3\n\t"
+        "s_xor_b32 %1, %1, %2\n\t"
+        "s_lshr_b32 %2, %4, 3\n\t"
+        "s_xor_b32 %0, %1, %2"
+        : "=s"(r), "=&s"(t0), "=&s"(t1), "=&s"(t2)
+        : "s"(x)
+        : "scc");
+    return r;
+}
+
+// A launch constant (kernarg SGPR) copied once into a VGPR, so the inner
+// loop's ops that use it read no SGPR and stay in the fast class.
+BM_DEV uint32_t vgpr_copy(uint32_t x) {
+    uint32_t r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+    return r;
+}
+
 // Inner-loop rounds [R0, 64) of the last block, with two shortcuts
 // (BM_FOLD, A/B-able):
 //  * sigma0(W[V]) enters W[V+15]; V is the word that varies per nonce.  There
@@ -306,6 +339,9 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
     // (tools/check_inner.py).
     constexpr bool kFold = BM_FOLD && !PADB && LW >= 1 && !(NBV == 1 && (P == 53 || P == 54)) &&
                            !(NBV == 2 && P >= 17);
+    // BM_PIN (SALU sigma0 of the uniform digits, launch constants in VGPRs):
+    // not for P >= 48, where the extra VGPRs push the inner loop into scratch
+    constexpr bool kPin = BM_PIN && kFold && !(NBV == 1 && P >= 48);
 
     // Inner-loop digit steps: digit i (< ms) of the inner counter sits at
     // bit 8*(3 - P%4 + i) of word LW.
@@ -358,7 +394,7 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
                 } else {
                     constexpr int64_t c = tail_word<P, PADB>(k);
                     if constexpr (c < 0)
-                        wb[k] = A.tmpl[BOFF + k];
+                        wb[k] = (kPin && NBV == 1) ? vgpr_copy(A.tmpl[BOFF + k]) : A.tmpl[BOFF + k];
                     else
                         wb[k] = (uint32_t)c;
                 }
@@ -385,6 +421,9 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
                 }
                 const uint32_t wl = wo[LW];
                 const uint32_t s0wl = ssig0(wl);  // sigma0 of word LW's task part (kFold)
+                // BM_PIN: the round-63 constant and h1's midstate word as VGPRs
+                const uint32_t h0_add = (kPin && NBV == 1) ? vgpr_copy(st[0]) : st[0];
+                const uint32_t h1_add = (kPin && NBV == 1) ? vgpr_copy(st[1]) : st[1];
 
                 // ---- inner loop over the uniform low digit(s) of word LW ----
                 uint32_t J = 0, c0 = 0, c1 = 0, c2 = 0;
@@ -399,8 +438,9 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
 
                     uint32_t h0, h1;
                     if constexpr (kFold) {
-                        h0 = sha_rounds_h0<LW, LW>(x, w, s0wl ^ ssig0_uniform(J), st[0]);
-                        h1 = st[1] + x[1];
+                        const uint32_t s0J = kPin ? ssig0_salu(J) : ssig0_uniform(J);
+                        h0 = sha_rounds_h0<LW, LW>(x, w, s0wl ^ s0J, h0_add);
+                        h1 = h1_add + x[1];
                     } else if constexpr (PADB) {
                         sha_rounds<LW, 64>(x, w);
                         uint32_t y[8];

@@ -187,6 +187,127 @@ def split_add3(lines, kernels, every):
     return out, n
 
 
+# Ops cluster_runs may move: single-destination VALU (no carry, no VCC/EXEC
+# side effects) and SALU arithmetic (which writes SCC).  Anything else fences.
+CLUSTER_VALU = {"v_alignbit_b32", "v_bitop3_b32", "v_add_u32_e32", "v_add3_u32", "v_lshrrev_b32_e32",
+                "v_xor_b32_e32", "v_xad_u32", "v_or_b32_e32", "v_and_b32_e32", "v_mov_b32_e32", "v_sub_u32_e32",
+                "v_lshlrev_b32_e32", "v_perm_b32", "v_bfi_b32", "v_or3_b32", "v_xor3_b32", "v_lshl_or_b32",
+                "v_lshl_add_u32", "v_add_lshl_u32", "v_and_or_b32", "v_not_b32_e32"}
+CLUSTER_SALU_SCC = {"s_lshr_b32", "s_lshl_b32", "s_or_b32", "s_xor_b32", "s_and_b32", "s_add_i32", "s_add_u32",
+                    "s_sub_i32", "s_sub_u32"}
+CLUSTER_SALU = {"s_mov_b32", "s_movk_i32"} | CLUSTER_SALU_SCC
+REG_TOK = re.compile(r"\b([vs])(\d+)\b|\b([vs])\[(\d+):(\d+)\]")
+
+
+def _regs(text):
+    out = set()
+    for m in REG_TOK.finditer(text):
+        if m.group(1):
+            out.add(f"{m.group(1)}{m.group(2)}")
+        else:
+            out.update(f"{m.group(3)}{k}" for k in range(int(m.group(4)), int(m.group(5)) + 1))
+    return out
+
+
+def _defs_uses(line):
+    """(mnemonic, defs, uses) of a movable instruction, or None (a fence)."""
+    m = re.match(r"^\s+([sv]_[a-z0-9_]+)\s+(.*)$", line)
+    if not m or m.group(1) not in CLUSTER_VALU | CLUSTER_SALU:
+        return None
+    ops = _operands(m.group(2))
+    if len(ops) < 2:
+        return None
+    defs = _regs(ops[0])
+    uses = set().union(*(_regs(o) for o in ops[1:]))
+    if m.group(1) in CLUSTER_SALU_SCC:
+        defs.add("scc")
+    return m.group(1), defs, uses
+
+
+def _schedule(seg, max_run):
+    """Reorder one fence-free segment: a list schedule over its register
+    dependences (RAW, WAR, WAW, SCC) that keeps issuing VALU of the current
+    class (slow / fast) while any is ready, up to max_run in a row, then
+    switches; SALU goes as soon as it is ready; ties go to program order."""
+    n = len(seg)
+    succ = [[] for _ in range(n)]
+    indeg = [0] * n
+    last_def, readers = {}, {}
+
+    def edge(a, b):
+        if a != b:
+            succ[a].append(b)
+            indeg[b] += 1
+
+    info = []
+    for i, ln in enumerate(seg):
+        mn, defs, uses = _defs_uses(ln)
+        rest = ln.split(None, 1)[1] if len(ln.split(None, 1)) > 1 else ""
+        cls = "N" if mn.startswith("s_") else classify(mn, rest)
+        info.append(cls)
+        for r in uses:
+            if r in last_def:
+                edge(last_def[r], i)
+        for r in defs:
+            if r in last_def:
+                edge(last_def[r], i)
+            for u in readers.get(r, ()):
+                edge(u, i)
+        for r in uses:
+            readers.setdefault(r, []).append(i)
+        for r in defs:
+            last_def[r] = i
+            readers[r] = []
+    import heapq
+    ready = [i for i in range(n) if indeg[i] == 0]
+    heapq.heapify(ready)
+    order, cur, run = [], None, 0
+    while ready:
+        pool = sorted(ready)
+        pick = next((i for i in pool if info[i] == "N"), None)
+        if pick is None:
+            same = [i for i in pool if info[i] == cur] if (cur and (max_run <= 0 or run < max_run)) else []
+            pick = same[0] if same else pool[0]
+            if info[pick] != cur:
+                cur, run = info[pick], 0
+            run += 1
+        ready.remove(pick)
+        heapq.heapify(ready)
+        order.append(pick)
+        for j in succ[pick]:
+            indeg[j] -= 1
+            if indeg[j] == 0:
+                heapq.heappush(ready, j)
+    assert len(order) == n, "dependence cycle"
+    return [seg[i] for i in order]
+
+
+def cluster_runs(lines, kernels, max_run=0, min_valu=64):
+    """Reorder the straight-line stretches of the search kernels' big blocks
+    (>= min_valu VALU between fences) so slow and fast VALU come in longer
+    runs: fewer s_setprio toggles, longer phases for the arbiter to pair."""
+    out, in_kernel, seg = [], False, []
+
+    def flush():
+        nv = sum(1 for ln in seg if ln.lstrip().startswith("v_"))
+        out.extend(_schedule(seg, max_run) if nv >= min_valu else seg)
+        seg.clear()
+
+    for ln in lines:
+        m_fn = re.match(r"^(_Z\S+):", ln)
+        if m_fn:
+            in_kernel = any(k in m_fn.group(1) for k in kernels)
+        elif ln.startswith(".Lfunc_end"):
+            in_kernel = False
+        if in_kernel and _defs_uses(ln) is not None:
+            seg.append(ln)
+            continue
+        flush()
+        out.append(ln)
+    flush()
+    return out
+
+
 def run(lines, kernels, slow, fast, min_fast_run=1):
     """Insert the toggles.  A fast run shorter than min_fast_run VALU (counted
     up to the next label) keeps the slow priority."""
@@ -240,6 +361,9 @@ def main():
     ap.add_argument("--fold-sgpr", type=int, default=1, help="1: literal-fold known SGPR constants, split add3")
     ap.add_argument("--split-add3-every", type=int, default=0,
                     help="K > 0: split every K-th all-VGPR v_add3_u32 into two v_add_u32")
+    ap.add_argument("--cluster", type=int, default=-1,
+                    help=">= 0: reorder big blocks into longer slow / fast runs (0: unbounded runs, "
+                         "K: at most K in a row); -1: off")
     a = ap.parse_args()
     lines = open(a.src).readlines()
     if a.fold_sgpr:
@@ -248,6 +372,8 @@ def main():
     if a.split_add3_every:
         lines, n_split3 = split_add3(lines, a.kernels.split(","), a.split_add3_every)
         print(f"bm_prio: {a.src}: {n_split3} all-VGPR v_add3 split", file=sys.stderr)
+    if a.cluster >= 0:
+        lines = cluster_runs(lines, a.kernels.split(","), max_run=a.cluster)
     out, n_toggle, n_valu = run(lines, a.kernels.split(","), a.slow_prio, a.fast_prio, a.min_fast_run)
     open(a.dst, "w").writelines(out)
     print(f"bm_prio: {a.src}: {n_toggle} s_setprio over {n_valu} VALU", file=sys.stderr)
