@@ -4,7 +4,10 @@ into profiles/<round>/pmc_summary.json, per kernel: counters summed per
 dispatch and averaged over dispatches, HBM bytes per launch
 (FETCH_SIZE + WRITE_SIZE, KB -> bytes; MI355X_MICROARCH.md §HBM), the
 effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration) and VALU issue rate.
-Usage: pmc_summary.py <out_dir> [gpurun_out]"""
+Usage: pmc_summary.py <out_dir> [gpurun_out] [config]
+With a config (C2, C3 ...) only the passes under <gpurun_out>/pmc_<config>_*
+are read and the summary is written as pmc_summary_<config>.json (what
+bench.py looks up for that config's roofline fields)."""
 import collections
 import csv
 import glob
@@ -14,9 +17,10 @@ import sys
 
 out_dir = sys.argv[1]
 src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out"
+cfg = sys.argv[3] if len(sys.argv) > 3 else None
 per = collections.defaultdict(lambda: collections.defaultdict(dict))  # kernel -> dispatch -> counter
 dur = collections.defaultdict(dict)
-for f in glob.glob(os.path.join(src, "pmc_*", "*_counter_collection.csv")):
+for f in glob.glob(os.path.join(src, f"pmc_{cfg}_*" if cfg else "pmc_*", "*_counter_collection.csv")):
     tag = os.path.basename(os.path.dirname(f))
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
@@ -49,6 +53,6 @@ for k, disp in per.items():
             e["simd_cycles_per_valu"] = (m["GRBM_GUI_ACTIVE"] / 8) * 1024 / m["SQ_INSTS_VALU"]
     res[k] = e
 os.makedirs(out_dir, exist_ok=True)
-json.dump(res, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
+json.dump(res, open(os.path.join(out_dir, f"pmc_summary_{cfg}.json" if cfg else "pmc_summary.json"), "w"), indent=1)
 for k, e in res.items():
     print(k[:60], {x: (round(y, 3) if isinstance(y, float) else y) for x, y in e.items() if x != "counters"})
