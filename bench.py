@@ -339,8 +339,12 @@ def main():
     def step():
         res = search(msg, lo, hi)
         st = ctx.last_stats()
-        dom = max((st.launch[i] for i in range(st.recorded)), key=lambda L: L.nonces, default=None)
-        return res, dom
+        launches = [st.launch[i] for i in range(st.recorded)]
+        dom = max(launches, key=lambda L: L.nonces, default=None)
+        # this device's algorithmic ops over the call's GPU span (first
+        # launch start to last launch end): launches overlap on two streams
+        ops = sum(L.nonces * (L.nbv + L.pad_block) for L in launches) * OPS_PER_COMPRESSION
+        return res, (dom, ops, st.span_ms)
 
     for _ in range(args.warmup):
         step()
@@ -358,7 +362,8 @@ def main():
     total = hi - lo + 1
     value = total * args.steps / dt / 1e9
     want = golden(msg, lo, hi)
-    dom = doms[-1]
+    dom = doms[-1][0]
+    calls = [(o, sp) for _, o, sp in doms if sp > 0]
     out = {
         "metric": METRIC,
         "value": round(value, 4),
@@ -380,7 +385,7 @@ def main():
         "hip_runtime": hip_runtimes(),
     }
     if dom is not None:
-        ms = [d.ms for d in doms if d is not None]
+        ms = [d[0].ms for d in doms if d[0] is not None]
         dom_ms = sum(ms) / len(ms)
         c_eff = dom.nbv + dom.pad_block  # blocks the kernel compresses per nonce
         c_survey = compressions_per_nonce(len(msg), dom.digits)
@@ -416,6 +421,14 @@ def main():
             if ib:
                 ib["frac"] = round(dom.nonces / (dom_ms * 1e-3) / 1e9 / ib["GHs_per_gpu"], 4)
                 roof["issue_bound"] = ib
+        if calls:
+            # the whole call on this device: every launch's algorithmic ops over
+            # the span of its launches (two streams overlap launches, which
+            # stretches each launch's own event time)
+            span = sum(sp for _, sp in calls) / len(calls)
+            ach = sum(o for o, _ in calls) / len(calls) / (span * 1e-3) / 1e12
+            roof["call"] = {"achieved": round(ach, 3), "frac": round(ach / VALU_PEAK_T, 4), "span_ms": round(span, 3),
+                            "launches": ctx.last_stats().launches}
         out["roofline"] = roof
     if args.rehearse_one_gpu:
         out["rehearsal"] = "every rank / device is GPU 0: checks the multi-GPU split and combine, not a measurement"

@@ -300,3 +300,202 @@ def test_garbage_datagrams_do_not_stop_endpoints():
     c.Close()
     stop.set()
     srv.Close()
+
+
+# ---- lsp2_test.go:330-474: window max-capacity and scattered messages ----
+
+def _reader(read_fn, sink, stop):
+    def go():
+        while not stop.is_set():
+            try:
+                sink.append(read_fn())
+            except lsp.LSPError:
+                return
+    t = threading.Thread(target=go, daemon=True)
+    t.start()
+    return t
+
+
+@pytest.mark.parametrize("nclients,nmsgs,w", [(1, 5, 2), (3, 8, 3), (2, 12, 5)])
+def test_window_max_capacity(nclients, nmsgs, w):
+    """lsp2_test.go:330-395.  (1) Every server write dropped (no Acks): each
+    client's stream of nmsgs > w Data puts only w on the wire, so the server
+    reads exactly w per client; with writes back on, it reads the rest, in
+    order.  (2) The same with every client write dropped, server -> clients."""
+    p = params(w=w, ms=40, k=200)
+    srv = lsp.NewServer(0, p)
+    clients = [lsp.NewClient(f"127.0.0.1:{srv.port}", p) for _ in range(nclients)]
+    stop = threading.Event()
+    got = []
+    _reader(srv.Read, got, stop)
+    # (1) client -> server
+    lspnet.SetServerWriteDropPercent(100)
+    for k, c in enumerate(clients):
+        for i in range(nmsgs):
+            c.Write(f"c{k}-{i}".encode())
+    time.sleep(0.3)
+    assert len(got) == w * nclients, got
+    lspnet.SetServerWriteDropPercent(0)
+    deadline = time.monotonic() + 10
+    while len(got) < nmsgs * nclients and time.monotonic() < deadline:
+        time.sleep(0.02)
+    for c in clients:
+        cid = c.ConnID()
+        k = clients.index(c)
+        assert [d for i, d in got if i == cid] == [f"c{k}-{i}".encode() for i in range(nmsgs)]
+    # (2) server -> client
+    lspnet.SetClientWriteDropPercent(100)
+    sinks = [[] for _ in clients]
+    for c, s in zip(clients, sinks):
+        _reader(c.Read, s, stop)
+    for c in clients:
+        for i in range(nmsgs):
+            srv.Write(c.ConnID(), f"s{c.ConnID()}-{i}".encode())
+    time.sleep(0.3)
+    assert [len(s) for s in sinks] == [w] * nclients
+    lspnet.SetClientWriteDropPercent(0)
+    deadline = time.monotonic() + 10
+    while any(len(s) < nmsgs for s in sinks) and time.monotonic() < deadline:
+        time.sleep(0.02)
+    for c, s in zip(clients, sinks):
+        assert s == [f"s{c.ConnID()}-{i}".encode() for i in range(nmsgs)]
+    stop.set()
+    for c in clients:
+        c.Close()
+    srv.Close()
+
+
+@pytest.mark.parametrize("nclients,nmsgs,w", [(1, 4, 8), (3, 6, 10)])
+def test_window_scattered_messages(nclients, nmsgs, w):
+    """lsp2_test.go:397-474.  With w > nmsgs, the first half of a stream is
+    written while every client write is dropped and the second half after:
+    the receiver still delivers all of it in order (the first half is re-sent
+    at the next epochs).  Then the same from the server to the clients."""
+    p = params(w=w, ms=40, k=200)
+    srv = lsp.NewServer(0, p)
+    clients = [lsp.NewClient(f"127.0.0.1:{srv.port}", p) for _ in range(nclients)]
+    half = nmsgs // 2
+    lspnet.SetClientWriteDropPercent(100)
+    for k, c in enumerate(clients):
+        for i in range(half):
+            c.Write(f"c{k}-{i}".encode())
+    lspnet.SetClientWriteDropPercent(0)
+    for k, c in enumerate(clients):
+        for i in range(half, nmsgs):
+            c.Write(f"c{k}-{i}".encode())
+    got = [srv.Read() for _ in range(nmsgs * nclients)]
+    for k, c in enumerate(clients):
+        assert [d for i, d in got if i == c.ConnID()] == [f"c{k}-{i}".encode() for i in range(nmsgs)]
+    lspnet.SetServerWriteDropPercent(100)
+    for c in clients:
+        for i in range(half):
+            srv.Write(c.ConnID(), f"s-{i}".encode())
+    lspnet.SetServerWriteDropPercent(0)
+    for c in clients:
+        for i in range(half, nmsgs):
+            srv.Write(c.ConnID(), f"s-{i}".encode())
+    for c in clients:
+        assert [c.Read() for _ in range(nmsgs)] == [f"s-{i}".encode() for i in range(nmsgs)]
+    for c in clients:
+        c.Close()
+    srv.Close()
+
+
+# ---- lsp4_test.go:113-140, 380-442: network toggled off while streams are written ----
+
+@pytest.mark.parametrize("mode", ["server_to_client", "client_to_server", "round_trip"])
+@pytest.mark.parametrize("nclients,nmsgs", [(1, 10), (3, 10), (5, 60)])
+def test_network_toggling(mode, nclients, nmsgs):
+    """All writes of one direction happen while the network is off (global
+    write drop 100%, as runNetwork does); the network comes back within K
+    epochs and every message arrives, in order, within the reference's epoch
+    budget (setMaxEpochs 12-20)."""
+    p = params(w=1, ms=50, k=5)
+    srv = lsp.NewServer(0, p)
+    clients = [lsp.NewClient(f"127.0.0.1:{srv.port}", p) for _ in range(nclients)]
+    budget = time.monotonic() + 20 * p.EpochMillis / 1000.0 + nmsgs * nclients * 0.01
+    want = {c.ConnID(): [f"{c.ConnID()}:{i}".encode() for i in range(nmsgs)] for c in clients}
+
+    def off_then_on(write_all):
+        lspnet.SetWriteDropPercent(100)
+        write_all()
+        time.sleep(p.EpochMillis / 1000.0)  # well inside K epochs of silence
+        lspnet.SetWriteDropPercent(0)
+
+    if mode in ("client_to_server", "round_trip"):
+        off_then_on(lambda: [c.Write(m) for c in clients for m in want[c.ConnID()]])
+        got = {}
+        for _ in range(nmsgs * nclients):
+            cid, d = srv.Read()
+            got.setdefault(cid, []).append(d)
+        assert got == want
+        if mode == "round_trip":  # echo everything back while the network is off
+            off_then_on(lambda: [srv.Write(cid, d) for cid, ds in got.items() for d in ds])
+    if mode == "server_to_client":
+        off_then_on(lambda: [srv.Write(cid, m) for cid, ms in want.items() for m in ms])
+    if mode in ("server_to_client", "round_trip"):
+        for c in clients:
+            assert [c.Read() for _ in range(nmsgs)] == want[c.ConnID()]
+    assert time.monotonic() < budget, "messages arrived after the epoch budget"
+    for c in clients:
+        c.Close()
+    srv.Close()
+
+
+# ---- lsp3_test.go:175-320: close semantics after an echo phase ----
+
+def _echo_phase(srv, clients, nmsgs):
+    for k, c in enumerate(clients):
+        for i in range(nmsgs):
+            c.Write(f"{k}.{i}".encode())
+    for _ in range(nmsgs * len(clients)):
+        cid, d = srv.Read()
+        srv.Write(cid, d)
+    for k, c in enumerate(clients):
+        assert [c.Read() for _ in range(nmsgs)] == [f"{k}.{i}".encode() for i in range(nmsgs)]
+
+
+@pytest.mark.parametrize("nclients", [1, 3])
+def test_server_close_conns(nclients):
+    """TestServerCloseConns: after echoing, the server CloseConn()s every
+    client; each client's next Read reports the connection lost."""
+    p = params(w=1, ms=30, k=5)
+    srv = lsp.NewServer(0, p)
+    clients = [lsp.NewClient(f"127.0.0.1:{srv.port}", p) for _ in range(nclients)]
+    _echo_phase(srv, clients, 5)
+    for c in clients:
+        srv.CloseConn(c.ConnID())
+    t0 = time.monotonic()
+    for c in clients:
+        with pytest.raises(lsp.LSPError):
+            c.Read()
+    assert time.monotonic() - t0 < 20 * p.EpochMillis / 1000.0
+    for c in clients:
+        c.Close()
+    srv.Close()
+
+
+@pytest.mark.parametrize("nclients", [1, 3])
+def test_client_close(nclients):
+    """TestClientClose: after echoing, every client Close()s; the server's
+    Read reports one lost connection per client, then keeps serving."""
+    p = params(w=1, ms=30, k=5)
+    srv = lsp.NewServer(0, p)
+    clients = [lsp.NewClient(f"127.0.0.1:{srv.port}", p) for _ in range(nclients)]
+    _echo_phase(srv, clients, 5)
+    ids = {c.ConnID() for c in clients}
+    for c in clients:
+        c.Close()
+    dead = set()
+    t0 = time.monotonic()
+    while dead != ids:
+        with pytest.raises(lsp.LSPError) as ei:
+            srv.Read()
+        dead.add(ei.value.conn_id)
+        assert time.monotonic() - t0 < 20 * p.EpochMillis / 1000.0
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", p)  # a new client still gets service
+    c.Write(b"again")
+    cid, d = srv.Read()
+    assert (cid, d) == (c.ConnID(), b"again")
+    c.Close()
+    srv.Close()
