@@ -290,8 +290,26 @@ def open_contexts(args, world, rank, local):
                 how += " [rehearsal: every rank on GPU 0]"
             return ctx, grp, search, how
         uid = grp.rdzv.broadcast_bytes(rccl_unique_id() if grp.rank == 0 else None)
-        ctx = Context(devices=[local], rank=grp.rank, world=grp.world, unique_id=uid)
-        return ctx, grp, ctx.search, f"{world} processes (one per GPU), RCCL allgather of 16 B partials in-library"
+        ctx, err = None, None
+        try:
+            ctx = Context(devices=[local], rank=grp.rank, world=grp.world, unique_id=uid)
+        except _lib.BtcMinerError as e:
+            err = str(e)
+        errs = [x for x in grp.gather(err) if x]
+        if not errs:
+            return ctx, grp, ctx.search, f"{world} processes (one per GPU), RCCL allgather of 16 B partials in-library"
+        # every rank saw the failure: fall back to gathering the partials over
+        # the rendezvous (the measurement is the same search; the combine is 16 B)
+        log(f"rank {grp.rank}: RCCL group failed ({errs[0]}); combining over gloo instead")
+        if ctx is not None:
+            ctx.close()
+        ctx = Context(devices=[local])
+
+        def search(msg, lo, hi):
+            piece = rank_piece(lo, hi, grp.rank, grp.world)
+            part = ctx.search(msg, *piece) if piece else (U64, U64)
+            return lex_min(tuple(p) for p in grp.gather(list(part)))
+        return ctx, grp, search, f"{world} processes (one per GPU), gloo gather of 16 B partials (RCCL failed: {errs[0]})"
     grp = Group()
     n = args.gpus
     if n > 1:

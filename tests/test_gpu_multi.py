@@ -255,3 +255,47 @@ def test_split_range_matches_library(gpu_ctx):
         for i in range(st.recorded):
             per[st.launch[i].device] = per.get(st.launch[i].device, 0) + st.launch[i].nonces
     assert [per[i] for i in range(3)] == [b - a + 1 for a, b in split_range(lo, hi, 3)]
+
+
+_RANK_BOOT = r"""
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+from distributed_bitcoin_minter_amd import _lib
+_lib.load()
+from distributed_bitcoin_minter_amd import BtcMinerError, Context, rccl_unique_id
+from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
+with Rendezvous(timeout_s=120) as rz:
+    uid = rz.broadcast_bytes(rccl_unique_id() if rz.rank == 0 else None)
+    try:
+        with Context(devices=[0], rank=rz.rank, world=rz.world, unique_id=uid) as c:
+            status = 0
+    except BtcMinerError as e:
+        status = e.status
+    seen = rz.all_gather(status)
+print(json.dumps({"rank": rz.rank, "status": status, "seen": seen}))
+"""
+
+
+def test_rank_group_bootstrap_two_ranks_one_gpu():
+    """Two rank contexts on the SAME GPU: the unique id made by rank 0 reaches
+    rank 1 over the rendezvous, both join RCCL's bootstrap, and RCCL then
+    refuses the duplicate GPU -- both ranks get BM_ERCCL promptly (no hang),
+    which is what bench.py's fallback relies on.  (Two distinct GPUs would
+    form the group: the driver's multi-GPU run.)"""
+    import socket
+    from distributed_bitcoin_minter_amd._lib import BM_ERCCL
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", _RANK_BOOT, ROOT], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e[-3000:]
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    assert all(o["seen"] == [BM_ERCCL, BM_ERCCL] for o in outs), outs
