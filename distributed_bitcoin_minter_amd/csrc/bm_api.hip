@@ -27,7 +27,7 @@ namespace bm {
 static const void* g_search[2][64];
 
 constexpr int kMaxInnerDigits = 2;  // S <= 100 nonces per task: small dequeue chunks, short tail
-constexpr uint32_t kNoncesPerLaneChunk = 100;
+constexpr uint32_t kNoncesPerLaneChunk = 100;  // default nonces per lane per dequeue (BTCMINER_CHUNK)
 constexpr int kEventPairs = BM_MAX_LAUNCH_STATS;
 // Launch streams per device.  Every search launch is a persistent grid that
 // drains a work counter, so its last tasks leave CUs idle (about half a
@@ -101,6 +101,7 @@ struct bm_ctx {
     bool nccl_ready = false;
     int rank = 0, world = 1;  // bm_ctx_create_rank: this process's place in an RCCL process group
     int fault_after = -1;     // test hook: fail after enqueueing this many launches (-1: off)
+    uint64_t lane_chunk = bm::kNoncesPerLaneChunk;  // nonces per lane per dequeue, at most (BTCMINER_CHUNK)
     bm_stats_t stats;
 };
 
@@ -148,7 +149,7 @@ int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_
     const uint64_t T = t_end - t0;
     // Tasks per lane per dequeue: about 100 nonces, but at least ~8 dequeues
     // per resident lane so the launch drains evenly (small launches: 1).
-    const uint64_t m_max = std::max<uint64_t>(1, kNoncesPerLaneChunk / S);
+    const uint64_t m_max = std::max<uint64_t>(1, ctx->lane_chunk / S);
     const uint32_t m = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>(m_max, T / (8 * resident * (uint64_t)kBlock)));
     const uint64_t chunks = (T + 64ull * m - 1) / (64ull * m);
@@ -616,6 +617,12 @@ void read_env(bm_ctx* ctx) {
         errno = 0;
         const unsigned long long v = std::strtoull(e, &end, 10);
         if (end != e && *end == '\0' && errno == 0 && v <= kMaxTailNonces) ctx->tail_nonces = v;
+    }
+    if (const char* e = std::getenv("BTCMINER_CHUNK")) {
+        char* end = nullptr;
+        errno = 0;
+        const unsigned long long v = std::strtoull(e, &end, 10);
+        if (end != e && *end == '\0' && errno == 0 && v >= 10 && v <= 100000) ctx->lane_chunk = v;
     }
 }
 
