@@ -318,6 +318,9 @@ BM_DEV uint64_t readfirstlane_u64(uint64_t v) {
 constexpr int search_waves(int P, int NBV) {
     return (NBV == 1 && P >= 55) ? BM_WAVES_PAD : (NBV == 2 ? BM_WAVES_NBV2 : 8);
 }
+#ifndef BM_LDS_BEST  // a lane's running best (hash, nonce) kept in LDS, not in VGPRs (A/B knob)
+#define BM_LDS_BEST 0
+#endif
 #ifndef BM_KATTR  // occupancy request of the search kernels (a build knob; see Makefile)
 #define BM_KATTR __attribute__((amdgpu_waves_per_eu(search_waves(P, NBV), 8)))
 #endif
@@ -352,6 +355,14 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
 
     uint64_t best_h = ~0ull, best_n = ~0ull;
     uint32_t bh = 0xFFFFFFFFu;  // high word of best_h
+#if BM_LDS_BEST
+    // The full 64-bit best and its nonce are touched only on the rare path
+    // (a new low); in LDS they cost no VGPRs, so no spill slots and no scratch
+    // stores on that path.  Only bh stays in a register for the compare.
+    __shared__ uint64_t lbest_h[kBlock], lbest_n[kBlock];
+    lbest_h[threadIdx.x] = ~0ull;
+    lbest_n[threadIdx.x] = ~0ull;
+#endif
 
     const uint32_t S = A.S;
     // TWOW: S in {10, 100} = n_out x 10; otherwise one pass of S inner steps
@@ -361,12 +372,21 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
     const uint64_t ntask = A.t_end - A.t0;
     const uint64_t chunk = 64ull * A.chunk_m;
 
+    uint64_t rem = ntask;  // tasks left as of this wave's last dequeue (guided sizing)
     for (;;) {
+        // guided: big chunks while much is left, one task per lane at the end
+        // (fewer returning atomics, the same fine drain); wave-uniform
+        uint32_t m = A.chunk_m;
+        if (A.guide_shift) {
+            const uint64_t g = rem >> A.guide_shift;
+            m = (uint32_t)(g < 1 ? 1 : (g < (uint64_t)A.chunk_m ? g : A.chunk_m));
+        }
         uint64_t base = 0;
-        if (lane == 0) base = atomicAdd(counter, (unsigned long long)chunk);
+        if (lane == 0) base = atomicAdd(counter, (unsigned long long)(A.guide_shift ? 64ull * m : chunk));
         base = readfirstlane_u64(base);
         if (base >= ntask) break;
-        for (uint32_t i = 0; i < A.chunk_m; ++i) {
+        rem = ntask - base;
+        for (uint32_t i = 0; i < m; ++i) {
             const uint64_t tt = base + 64ull * i + lane;
             if (tt >= ntask) break;
             const uint64_t t = A.t0 + tt;
@@ -464,11 +484,19 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
                     if (__builtin_expect(h0 <= bh, 0)) {
                         const uint64_t h = ((uint64_t)h0 << 32) | h1;
                         const uint64_t v = vbase + (uint64_t)jo * n_in + j;
+#if BM_LDS_BEST
+                        if (h < lbest_h[threadIdx.x] && v >= A.vlo && v <= A.vhi) {
+                            lbest_h[threadIdx.x] = h;
+                            lbest_n[threadIdx.x] = A.nonce_base + v;
+                            bh = h0;
+                        }
+#else
                         if (h < best_h && v >= A.vlo && v <= A.vhi) {
                             best_h = h;
                             best_n = A.nonce_base + v;
                             bh = h0;
                         }
+#endif
                     }
 
                     // step the uniform decimal counter held in word LW
@@ -490,6 +518,10 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
         }
     }
 
+#if BM_LDS_BEST
+    best_h = lbest_h[threadIdx.x];
+    best_n = lbest_n[threadIdx.x];
+#endif
     if (block_min<kBlock>(best_h, best_n)) part[A.part_off + blockIdx.x] = Partial{best_h, best_n};
 }
 

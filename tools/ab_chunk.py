@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
-"""A/B the dequeue chunk (BTCMINER_CHUNK: nonces per lane per work-counter
-dequeue) on C2 and C3: one process, a fresh context per setting, settings
-alternated round after round; best-of-N wall time, answers checked against
-the goldens.  Results never depend on the knob.
+"""A/B a context-creation knob (default BTCMINER_CHUNK: nonces per lane per
+work-counter dequeue; --var BTCMINER_GUIDED ...) on C2 and C3: one process, a
+fresh context per setting, settings alternated round after round; best-of-N
+wall time, answers checked against the goldens.  Results never depend on the
+knob.  The library is BTCMINER_LIB (default: the in-tree build).
 
-    python tools/ab_chunk.py 100 400 1600 [--rounds 3] [--reps 5]"""
+    python tools/ab_chunk.py 100 400 1600 [--var BTCMINER_CHUNK] [--rounds 3] [--reps 5]"""
 import argparse
 import json
 import os
@@ -16,14 +17,15 @@ from distributed_bitcoin_minter_amd import Context  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("chunks", nargs="+", type=int)
+ap.add_argument("--var", default="BTCMINER_CHUNK")
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--reps", type=int, default=5)
 a = ap.parse_args()
 gold = {c["config"]: c for c in json.load(open(os.path.join(ROOT, "tests/golden/full_range.json")))["cases"]}
 for rnd in range(a.rounds):
     for ch in a.chunks:
-        os.environ["BTCMINER_CHUNK"] = str(ch)
-        out = {"round": rnd, "chunk": ch}
+        os.environ[a.var] = str(ch)
+        out = {"round": rnd, a.var: ch, "lib": os.path.basename(os.environ.get("BTCMINER_LIB", "libbtcminer.so"))}
         with Context(devices=[0]) as ctx:
             ctx.set_timing(True)
             for cfg in ("C2", "C3"):
