@@ -21,7 +21,11 @@ Outputs:
                     [0, 2^40-1], seed 0x5EED, scanned by the oracle's byte-string
                     loop (OpenSSL block code), not by bm_scan16.c
 
-Usage: python tests/golden/make_chunk_golden.py [--chunks K] [--threads T] [--windows]
+  c5_clients.json   (--c5) BASELINE C5's 16 client requests: msg "client-%02d",
+                    [0, 2^34-1] each, scanned by the AVX-512 scan (answers re-hashed
+                    with hashlib)
+
+Usage: python tests/golden/make_chunk_golden.py [--chunks K] [--threads T] [--windows] [--c5]
 """
 import argparse
 import hashlib
@@ -58,12 +62,34 @@ def main():
     ap.add_argument("--chunks", type=int, default=NCHUNK, help="compute chunks 0..K-1")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--windows", action="store_true", help="only (re)make c4_windows.json")
+    ap.add_argument("--c5", action="store_true", help="only (re)make c5_clients.json")
     args = ap.parse_args()
 
     import subprocess
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     from conftest import Oracle
     oracle = Oracle(os.path.join(ROOT, "oracle", "liboracle.so"))
+
+    if args.c5:
+        path = os.path.join(HERE, "c5_clients.json")
+        data = json.load(open(path)) if os.path.exists(path) else {
+            "config": "C5", "lower": 0, "upper": (1 << 34) - 1, "clients": {}}
+        data["generator"] = ("oracle/bm_scan16.c (16-lane AVX-512 scan, checked against oracle_search by "
+                             "tests/test_oracle.py); every answer re-hashed with hashlib")
+        for i in range(16):
+            msg = f"client-{i:02d}"
+            if msg in data["clients"]:
+                continue
+            t = time.time()
+            h, n = oracle.search_x16(msg.encode(), 0, (1 << 34) - 1, threads=args.threads)
+            assert ref_hash(msg.encode(), n) == h
+            data["clients"][msg] = [h, n]
+            with open(path + ".tmp", "w") as f:
+                json.dump(data, f, indent=0)
+                f.write("\n")
+            os.replace(path + ".tmp", path)
+            print(msg, h, n, f"{time.time() - t:.1f} s", flush=True)
+        return
 
     if args.windows:
         import random

@@ -93,6 +93,45 @@ def test_c5_gpu_miners_16_clients_10pct_drop(gpu_ctx, oracle):
     stop(bs, threads, gm)
 
 
+def test_c5_at_size_against_cpu_goldens():
+    """BASELINE C5 at its full size: 16 clients, each asking for [0, 2^34-1]
+    of "client-%02d", 2^32-nonce jobs (the server default), 4 GPU miners
+    sharing the box's GPU, 10% read and write drop at every endpoint.
+    Every answer equals a full CPU scan of that client's 2^34 nonces
+    (tests/golden/c5_clients.json, AVX-512 oracle)."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_clients.json")
+    if not os.path.exists(path):
+        pytest.skip("c5_clients.json not generated")
+    gold = json.load(open(path))
+    if len(gold["clients"]) < 16:
+        pytest.skip("c5_clients.json incomplete")
+    p = lsp.Params(EpochLimit=100, EpochMillis=50, WindowSize=1)
+    srv, bs, threads, gm = start(1 << 32, p, 4)
+    lspnet.SetReadDropPercent(10)
+    lspnet.SetWriteDropPercent(10)
+    msgs = [f"client-{i:02d}" for i in range(16)]
+    got = {}
+
+    def ask(i):
+        got[i] = client.request(f"127.0.0.1:{srv.port}", msgs[i], gold["upper"], p)
+
+    t0 = time.monotonic()
+    th = [threading.Thread(target=ask, args=(i,)) for i in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    secs = time.monotonic() - t0
+    lspnet.ResetDropPercent()
+    for i, m in enumerate(msgs):
+        assert got.get(i) == tuple(gold["clients"][m]), (m, got.get(i))
+    assert bs.stats["chunks_done"] >= 16 * 4
+    print(f"C5 at size: {16 << 34} nonces in {secs:.2f} s = {(16 << 34) / secs / 1e9:.2f} GH/s end to end")
+    stop(bs, threads, gm)
+
+
 def test_gpu_miner_failover():
     """A GPU miner dies mid-request; its chunk is redone by another."""
     p = lsp.Params(EpochLimit=5, EpochMillis=20, WindowSize=1)
