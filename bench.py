@@ -435,8 +435,18 @@ def main():
             roof["valu_dual_issued_frac_pmc"] = round(cnt["SQ_ACTIVE_INST_VALU2"] / cnt["SQ_INSTS_VALU"], 4)
         if clock:
             roof["clock_ghz_pmc"] = round(clock, 3)
-            ib = issue_bound(dom.p, dom.nbv, clock)
+        # the live clock under the dominant launch (s_memtime / s_memrealtime
+        # stamped by workgroup 0, averaged over the timed steps); the PMC clock
+        # of the committed profile otherwise (another run, maybe another box)
+        live = [d[0].clock_ghz for d in doms if d[0] is not None and d[0].clock_ghz > 0]
+        live_clock = sum(live) / len(live) if live else None
+        if live_clock:
+            roof["clock_ghz_live"] = round(live_clock, 3)
+        ib_clock = live_clock or clock
+        if ib_clock:
+            ib = issue_bound(dom.p, dom.nbv, ib_clock)
             if ib:
+                ib["clock_src"] = "live (s_memtime / s_memrealtime)" if live_clock else pmc_src
                 ib["frac"] = round(dom.nonces / (dom_ms * 1e-3) / 1e9 / ib["GHs_per_gpu"], 4)
                 roof["issue_bound"] = ib
         if calls:

@@ -36,7 +36,7 @@ class Result(ctypes.Structure):
 class LaunchStat(ctypes.Structure):
     _fields_ = [("device", c_i32), ("p", c_i32), ("nbv", c_i32), ("pad_block", c_i32), ("digits", c_i32),
                 ("inner_digits", c_i32), ("nonces", c_u64), ("grid", c_u32), ("tasks_per_thread", c_u32),
-                ("ms", ctypes.c_double)]
+                ("ms", ctypes.c_double), ("clock_ghz", ctypes.c_double)]
 
 
 class Stats(ctypes.Structure):

@@ -36,6 +36,7 @@ constexpr int kEventPairs = BM_MAX_LAUNCH_STATS;
 // workgroups fill the CUs the previous one frees.
 constexpr int kMaxStreams = 4;
 constexpr uint64_t kMaxTailNonces = 1ull << 40;
+constexpr size_t kCtrStride = 32;  // u64 words per launch: counter [0], clock stamps [16..19] (kClockSlot)
 
 struct DeviceCtx {
     int id = -1;
@@ -43,7 +44,9 @@ struct DeviceCtx {
     hipStream_t stream = nullptr;
     Partial* d_part = nullptr;
     size_t part_cap = 0;
-    unsigned long long* d_ctr = nullptr;  // one dequeue counter per launch
+    unsigned long long* d_ctr = nullptr;  // per launch a strip of kCtrStride words: [0] dequeue
+                                          // counter, [16..19] clock stamps (bm_kernels.hpp)
+    unsigned long long* h_ctr = nullptr;  // pinned copy of the strips (timing on)
     size_t ctr_cap = 0;
     Partial* d_result = nullptr;  // 1 partial
     Partial* d_gather = nullptr;  // nslots partials (allgather target)
@@ -57,6 +60,7 @@ struct DeviceCtx {
     hipEvent_t fork = nullptr, join[kMaxStreams - 1] = {};
     ncclComm_t comm = nullptr;  // multi-device ctx: ncclCommInitAll; rank ctx: the process group's
     std::vector<std::pair<const void*, int>> occ;  // kernel -> blocks per CU
+    double wall_clock_hz = 100e6;                  // s_memrealtime rate
 };
 
 struct Launch {
@@ -207,10 +211,13 @@ int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_
 int ensure_counters(DeviceCtx& d, size_t n) {
     if (n <= d.ctr_cap) return BM_OK;
     if (d.d_ctr) BM_HIP(hipFree(d.d_ctr));
+    if (d.h_ctr) BM_HIP(hipHostFree(d.h_ctr));
     d.d_ctr = nullptr;
+    d.h_ctr = nullptr;
     d.ctr_cap = 0;
     size_t cap = std::max<size_t>(n, 256);
-    BM_HIP(hipMalloc(&d.d_ctr, cap * sizeof(unsigned long long)));
+    BM_HIP(hipMalloc(&d.d_ctr, cap * kCtrStride * sizeof(unsigned long long)));
+    BM_HIP(hipHostMalloc(&d.h_ctr, cap * kCtrStride * sizeof(unsigned long long), hipHostMallocDefault));
     d.ctr_cap = cap;
     return BM_OK;
 }
@@ -235,6 +242,9 @@ int init_device(DeviceCtx& d, int id, int nslots) {
     BM_HIP(hipGetDeviceProperties(&prop, id));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return BM_ENODEV;  // kernels are gfx950 code objects
     d.cus = prop.multiProcessorCount;
+    int wall_khz = 0;
+    if (hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, id) == hipSuccess && wall_khz > 0)
+        d.wall_clock_hz = 1e3 * wall_khz;
     BM_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     BM_HIP(hipMalloc(&d.d_result, sizeof(Partial)));
     BM_HIP(hipMalloc(&d.d_gather, sizeof(Partial) * (size_t)nslots));
@@ -259,6 +269,7 @@ void destroy_device(DeviceCtx& d) {
         if (e) (void)hipEventDestroy(e);
     if (d.d_part) (void)hipFree(d.d_part);
     if (d.d_ctr) (void)hipFree(d.d_ctr);
+    if (d.h_ctr) (void)hipHostFree(d.h_ctr);
     if (d.d_result) (void)hipFree(d.d_result);
     if (d.d_gather) (void)hipFree(d.d_gather);
     if (d.d_hash_io) (void)hipFree(d.d_hash_io);
@@ -319,7 +330,8 @@ int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches,
         BM_HIP(hipSetDevice(d.id));
         uint32_t nparts = 0, li = 0;
         if (!launches[di].empty())
-            BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches[di].size() * sizeof(unsigned long long), d.stream));
+            BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches[di].size() * kCtrStride * sizeof(unsigned long long),
+                                  d.stream));
         // stream of each launch: biggest first, round-robin over the streams
         const int ns = std::max(1, std::min<int>(ctx->streams, (int)launches[di].size()));
         std::vector<uint32_t> order(launches[di].size());
@@ -339,7 +351,7 @@ int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches,
             if (ctx->fault_after >= 0 && enqueued == ctx->fault_after) return BM_EINTERNAL;  // test hook
             const bool timed = ctx->timing && li < (uint32_t)kEventPairs;
             if (timed) BM_HIP(hipEventRecord(d.ev[2 * li], s));
-            unsigned long long* ctr = d.d_ctr + li;
+            unsigned long long* ctr = d.d_ctr + kCtrStride * li;
             void* kargs[] = {&L.args, &d.d_part, &ctr};
             BM_HIP(hipLaunchKernel(L.fn, dim3(L.grid), dim3(kBlock), kargs, 0, s));
             ++enqueued;
@@ -353,6 +365,9 @@ int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches,
         // nparts = 0 (a device or rank with nothing to scan) writes (2^64-1, 2^64-1)
         reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, d.d_result);
         BM_HIP(hipGetLastError());
+        if (ctx->timing && !launches[di].empty())  // the clock stamps, for the launch statistics
+            BM_HIP(hipMemcpyAsync(d.h_ctr, d.d_ctr, launches[di].size() * kCtrStride * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, d.stream));
     }
 
     // 3. combine: one RCCL allgather of the 16-byte partials, or plain copies
@@ -493,6 +508,9 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
                 BM_HIP(hipEventElapsedTime(&ms, d.ev[2 * li], d.ev[2 * li + 1]));
                 L.stat.ms = ms;
                 st.kernel_ms += ms;
+                const unsigned long long* c = d.h_ctr + kCtrStride * li + kClockSlot - 1;
+                if (c[4] > c[2] && c[3] > c[1])  // shader cycles over constant-rate ticks
+                    L.stat.clock_ghz = (double)(c[3] - c[1]) / ((double)(c[4] - c[2]) / d.wall_clock_hz) / 1e9;
                 if (span_ok) {  // the first launch's start to this launch's end
                     float sp = 0.f;
                     BM_HIP(hipEventElapsedTime(&sp, d.ev[2 * first[di]], d.ev[2 * li + 1]));

@@ -321,6 +321,17 @@ constexpr int search_waves(int P, int NBV) {
 #ifndef BM_LDS_BEST  // a lane's running best (hash, nonce) kept in LDS, not in VGPRs (A/B knob)
 #define BM_LDS_BEST 0
 #endif
+// BM_CLOCK_PROBE=1: workgroup 0 stamps the clock counters of each launch, so
+// bm_launch_stat_t.clock_ghz reports the live shader clock.  Off by default:
+// although the inner loop is unchanged, the C2 kernel measured 0.35-0.67%
+// slower with it (profiles/r02/ab_probe*.log); build with
+// EXTRA_HIPFLAGS=-DBM_CLOCK_PROBE=1 to measure clocks.
+#ifndef BM_CLOCK_PROBE
+#define BM_CLOCK_PROBE 0
+#endif
+// The stamps sit 128 B after the launch's dequeue counter (counter[0]): a line
+// of their own, away from the one every wave's atomics hit.
+constexpr int kClockSlot = 16;
 #ifndef BM_KATTR  // occupancy request of the search kernels (a build knob; see Makefile)
 #define BM_KATTR __attribute__((amdgpu_waves_per_eu(search_waves(P, NBV), 8)))
 #endif
@@ -372,6 +383,14 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
     const uint64_t ntask = A.t_end - A.t0;
     const uint64_t chunk = 64ull * A.chunk_m;
 
+    // clock probe: workgroup 0 (which dequeues until the counter runs dry, so
+    // it spans the launch) stamps the shader-clock and constant-rate counters
+    // next to the launch's dequeue counter; the host turns them into the
+    // launch's average clock (bm_launch_stat_t.clock_ghz)
+    if (BM_CLOCK_PROBE && blockIdx.x == 0 && threadIdx.x == 0) {
+        counter[kClockSlot + 0] = __builtin_amdgcn_s_memtime();
+        counter[kClockSlot + 1] = __builtin_amdgcn_s_memrealtime();
+    }
     uint64_t rem = ntask;  // tasks left as of this wave's last dequeue (guided sizing)
     for (;;) {
         // guided: big chunks while much is left, one task per lane at the end
@@ -518,6 +537,10 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
         }
     }
 
+    if (BM_CLOCK_PROBE && blockIdx.x == 0 && threadIdx.x == 0) {
+        counter[kClockSlot + 2] = __builtin_amdgcn_s_memtime();
+        counter[kClockSlot + 3] = __builtin_amdgcn_s_memrealtime();
+    }
 #if BM_LDS_BEST
     best_h = lbest_h[threadIdx.x];
     best_n = lbest_n[threadIdx.x];

@@ -124,6 +124,9 @@ typedef struct bm_launch_stat {
     uint32_t grid;        /* workgroups launched (256 threads each) */
     uint32_t tasks_per_thread; /* approx. tasks per lane (dynamic dequeue) */
     double ms;            /* launch duration from HIP events on its stream (0 if timing off) */
+    double clock_ghz;     /* average shader clock over the launch: s_memtime cycles over
+                             s_memrealtime ticks stamped by workgroup 0 (timing on, and a
+                             library built with BM_CLOCK_PROBE=1; 0 otherwise) */
 } bm_launch_stat_t;
 
 typedef struct bm_stats {

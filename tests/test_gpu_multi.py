@@ -190,6 +190,9 @@ def test_stats_span_vs_sum(gpu_ctx):
         assert st.launches >= 10 and st.span_ms > 0
         assert st.span_ms <= st.wall_ms
         assert max(st.launch[i].ms for i in range(st.recorded)) <= st.span_ms + 1e-3
+        # the live clock probe (BM_CLOCK_PROBE builds only): a plausible shader clock
+        dom = max((st.launch[i] for i in range(st.recorded)), key=lambda L: L.nonces)
+        assert dom.clock_ghz == 0.0 or 1.0 < dom.clock_ghz < 3.0, dom.clock_ghz
     finally:
         gpu_ctx.set_timing(False)
 

@@ -11,9 +11,9 @@ over the miners with its fair-share scheduler; each miner is miner.run over
 its own bm_ctx (device i % visible GPUs: on a one-GPU box all four share it).
 Prints one JSON line: whole-system GH/s = all clients' nonces / wall time from
 the first request to the last answer, the same figure for the bare library
-on the same GPUs, and the checks available at this size: every answer
-re-hashes to itself (bm_hash_gpu), and two clients' answers equal one
-whole-range bm_search_gpu call.
+on the same GPUs, and the checks: every answer re-hashes to itself
+(bm_hash_gpu), two clients' answers equal one whole-range bm_search_gpu call,
+and every answer equals the full CPU scan in tests/golden/c5_clients.json.
 """
 import argparse
 import json
@@ -93,6 +93,13 @@ def main():
         dt = time.perf_counter() - t
         out["direct_ok"] = direct == [got.get(0), got.get(a.clients - 1)]
         out["library_GHs_same_gpus"] = round(2 * (top + 1) / dt / 1e9, 3)
+    gpath = os.path.join(ROOT, "tests", "golden", "c5_clients.json")
+    if os.path.exists(gpath):  # full CPU scans of each client's range (AVX-512 oracle)
+        gold = json.load(open(gpath))
+        if gold["upper"] == top:
+            out["golden_ok"] = all(tuple(gold["clients"][msgs[i]]) == got.get(i)
+                                   for i in range(a.clients) if msgs[i] in gold["clients"])
+            out["golden_checked"] = sum(1 for m in msgs if m in gold["clients"])
     for m in gminers:
         m.close()
     print(json.dumps(out), flush=True)
