@@ -18,10 +18,11 @@ How N GPUs are driven (--gpus N):
     group (bm_ctx_create_rank on LOCAL_RANK; rank 0's unique id travels over
     the rendezvous), every rank calls bm_search_gpu on the WHOLE range, scans
     its contiguous piece, and one RCCL allgather of the 16-byte partials gives
-    every rank the answer.  torch.distributed (gloo, CPU) runs only in a
-    sidecar process (distributed_bitcoin_minter_amd/rendezvous.py) for the
-    unique id, the barriers and the max over ranks, so this process maps one
-    HIP runtime, /opt/rocm's, the one the GPU test suite runs on.
+    every rank the answer.  The unique id, the barriers and the max over
+    ranks go through a file rendezvous on the node
+    (distributed_bitcoin_minter_amd/rendezvous.py): no torch in any rank, so
+    each process maps one HIP runtime, /opt/rocm's, the one the GPU test
+    suite runs on, and only the ranks themselves hold the GPUs.
   * no launcher, N > 1: ONE process drives N devices (BASELINE C4's design):
     a multi-device context splits the range and combines with
     ncclCommInitAll + ncclAllGather inside the library.  Fewer than N visible
@@ -275,9 +276,9 @@ def open_contexts(args, world, rank, local):
     if world > 1:
         from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
         grp = Group(Rendezvous())
-        if args.rehearse_one_gpu or args.combine == "gloo":
+        if args.rehearse_one_gpu or args.combine == "gather":
             # every rank scans its piece on its own context; the 16-byte
-            # partials are gathered over the gloo sidecar
+            # partials are gathered over the rendezvous
             dev = 0 if args.rehearse_one_gpu else local
             ctx = Context(devices=[dev])
 
@@ -285,7 +286,7 @@ def open_contexts(args, world, rank, local):
                 piece = rank_piece(lo, hi, grp.rank, grp.world)
                 part = ctx.search(msg, *piece) if piece else (U64, U64)
                 return lex_min(tuple(p) for p in grp.gather(list(part)))
-            how = f"{world} processes (one per GPU), gloo gather of 16 B partials"
+            how = f"{world} processes (one per GPU), rendezvous gather of 16 B partials"
             if args.rehearse_one_gpu:
                 how += " [rehearsal: every rank on GPU 0]"
             return ctx, grp, search, how
@@ -300,7 +301,7 @@ def open_contexts(args, world, rank, local):
             return ctx, grp, ctx.search, f"{world} processes (one per GPU), RCCL allgather of 16 B partials in-library"
         # every rank saw the failure: fall back to gathering the partials over
         # the rendezvous (the measurement is the same search; the combine is 16 B)
-        log(f"rank {grp.rank}: RCCL group failed ({errs[0]}); combining over gloo instead")
+        log(f"rank {grp.rank}: RCCL group failed ({errs[0]}); gathering the partials over the rendezvous instead")
         if ctx is not None:
             ctx.close()
         ctx = Context(devices=[local])
@@ -309,7 +310,8 @@ def open_contexts(args, world, rank, local):
             piece = rank_piece(lo, hi, grp.rank, grp.world)
             part = ctx.search(msg, *piece) if piece else (U64, U64)
             return lex_min(tuple(p) for p in grp.gather(list(part)))
-        return ctx, grp, search, f"{world} processes (one per GPU), gloo gather of 16 B partials (RCCL failed: {errs[0]})"
+        return ctx, grp, search, (f"{world} processes (one per GPU), rendezvous gather of 16 B partials "
+                                  f"(RCCL failed: {errs[0]})")
     grp = Group()
     n = args.gpus
     if n > 1:
@@ -333,8 +335,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4"])
-    ap.add_argument("--combine", default="rccl", choices=["rccl", "gloo"],
-                    help="torchrun ranks: in-library RCCL allgather (default) or gather over the gloo sidecar")
+    ap.add_argument("--combine", default="rccl", choices=["rccl", "gather"],
+                    help="torchrun ranks: in-library RCCL allgather (default) or a gather over the rendezvous")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N-way split on ONE GPU (all ranks / devices are GPU 0): exercises the multi-GPU "

@@ -7,7 +7,8 @@ lexicographic (hash, nonce) min, which equals the reference's sequential
 strict-'<' scan (miner.go:59-65).  Inside one process the
 same split is done by a multi-device bm_ctx with an RCCL allgather
 (csrc/bm_api.hip).  With torch.distributed's "nccl" backend (RCCL on ROCm)
-the gather runs over xGMI; "gloo" is used for CPU tests.
+the gather runs over xGMI.  bench.py's torchrun ranks use the library's own
+RCCL group instead (bm_ctx_create_rank, rendezvous.py), with no torch.
 """
 U64_MAX = (1 << 64) - 1
 

@@ -1,134 +1,103 @@
-"""Process-group rendezvous for one process per GPU, kept out of the GPU
-process.
+"""Process-group rendezvous for one process per GPU on one node, without
+torch and without touching the GPU.
 
-A rank of `torchrun` (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the
-environment) needs a side channel for three small things: rank 0's RCCL
-unique id (so every rank can join the library's RCCL communicator,
-bm_ctx_create_rank), barriers around a timed region, and a max over ranks of
-the elapsed time.  torch.distributed's gloo backend provides them, but
-importing torch maps torch's bundled HIP runtime next to the /opt/rocm one
-libbtcminer.so uses.  So torch runs in a sidecar child process that joins the
-gloo group as this rank and serves requests over a pipe (one JSON line each
-way); the GPU process itself never imports torch.
+A rank launched by `torchrun --nnodes=1` (RANK / WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT in the environment) needs a side channel for three small things:
+rank 0's RCCL unique id (so every rank can join the library's RCCL
+communicator, bm_ctx_create_rank), barriers around a timed region, and a max
+over ranks of the elapsed time.  The data path does not go through here: the
+per-rank 16-byte partials are combined by the library's RCCL allgather.
 
-The data path does not go through here: the per-rank 16-byte partials are
-combined by the library's own RCCL allgather.  `all_gather` exists for the
-one-GPU rehearsal (every rank on device 0, where RCCL cannot place two ranks
-on one GPU) and for CPU tests.
+Why not torch.distributed: importing torch maps torch's own HIP runtime, and
+on this image it opens the GPU (a gloo sidecar per rank doubled the processes
+holding the GPU: 8 ranks + 8 sidecars + the launcher exceeded the box's
+16-process guard).  The ranks of one node share a filesystem, so each
+collective is a set of small files: rank r writes `<seq>.<r>` (atomically,
+by rename) and every rank waits until all `world` files of that step exist.
+The directory is keyed by MASTER_ADDR, MASTER_PORT and the launcher's pid (all
+ranks of one torchrun launch share their parent), and rank 0 removes it once
+every rank has left.
+
+`all_gather` also carries the partials for the one-GPU rehearsal (every rank
+on device 0, where RCCL cannot place two ranks on one GPU) and for CPU tests.
 """
 import json
 import os
-import subprocess
-import sys
-
-_HERE = os.path.dirname(os.path.abspath(__file__))
+import shutil
+import tempfile
+import time
 
 
 class Rendezvous:
-    """The calling process's seat in the torchrun group (env://, gloo)."""
+    """The calling process's seat in the group of one node's ranks."""
 
-    def __init__(self, timeout_s: float = 600.0):
+    def __init__(self, timeout_s: float = 600.0, path: str = None):
         self.rank = int(os.environ["RANK"])
         self.world = int(os.environ["WORLD_SIZE"])
-        env = dict(os.environ)
-        env["PYTHONPATH"] = os.path.dirname(_HERE) + os.pathsep + env.get("PYTHONPATH", "")
-        self._p = subprocess.Popen([sys.executable, "-u", "-m", "distributed_bitcoin_minter_amd.rendezvous",
-                                    str(timeout_s)], stdin=subprocess.PIPE, stdout=subprocess.PIPE, env=env,
-                                   text=True, bufsize=1)
-        self._call("ready")
+        self.timeout_s = timeout_s
+        key = f"{os.environ.get('MASTER_ADDR', 'local')}-{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}"
+        self.path = path or os.environ.get("BTCMINER_RDZV_DIR") or os.path.join(
+            tempfile.gettempdir(), f"btcminer-rdzv-{key}")
+        os.makedirs(self.path, exist_ok=True)
+        self._seq = 0
+        self._open = True
+        self.barrier()
 
-    def _call(self, op, value=None):
-        self._p.stdin.write(json.dumps({"op": op, "value": value}) + "\n")
-        self._p.stdin.flush()
-        line = self._p.stdout.readline()
-        if not line:
-            raise RuntimeError(f"rendezvous sidecar of rank {self.rank} exited (code {self._p.poll()})")
-        out = json.loads(line)
-        if "error" in out:
-            raise RuntimeError(f"rendezvous {op}: {out['error']}")
-        return out.get("value")
+    def _wait(self, names):
+        deadline = time.monotonic() + self.timeout_s
+        pause = 5e-5
+        while True:
+            if all(os.path.exists(n) for n in names):
+                return
+            if time.monotonic() > deadline:
+                missing = [os.path.basename(n) for n in names if not os.path.exists(n)]
+                raise RuntimeError(f"rendezvous {self.path}: rank {self.rank} timed out waiting for {missing}")
+            time.sleep(pause)
+            pause = min(pause * 2, 1e-3)
 
-    def broadcast_bytes(self, data: bytes = None, src: int = 0) -> bytes:
-        """src's bytes on every rank."""
-        return bytes.fromhex(self._call("bcast", data.hex() if self.rank == src else None))
-
-    def barrier(self):
-        self._call("barrier")
-
-    def all_max(self, x: float) -> float:
-        return self._call("max", float(x))
+    def _post(self, name, obj):
+        tmp = os.path.join(self.path, f".{name}.tmp")
+        with open(tmp, "w") as f:
+            json.dump(obj, f)
+        os.replace(tmp, os.path.join(self.path, name))
 
     def all_gather(self, obj):
         """List of every rank's JSON-able obj, by rank."""
-        return self._call("gather", obj)
+        if not self._open:
+            raise RuntimeError("rendezvous closed")
+        seq = self._seq
+        self._seq += 1
+        self._post(f"{seq}.{self.rank}", obj)
+        names = [os.path.join(self.path, f"{seq}.{r}") for r in range(self.world)]
+        self._wait(names)
+        out = []
+        for n in names:
+            with open(n) as f:
+                out.append(json.load(f))
+        return out
+
+    def broadcast_bytes(self, data: bytes = None, src: int = 0) -> bytes:
+        """src's bytes on every rank."""
+        return bytes.fromhex(self.all_gather(data.hex() if self.rank == src else None)[src])
+
+    def barrier(self):
+        self.all_gather(None)
+
+    def all_max(self, x: float) -> float:
+        return max(self.all_gather(float(x)))
 
     def close(self):
-        if self._p is None:
+        if not self._open:
             return
-        try:
-            self._call("close")
-        except (RuntimeError, OSError, ValueError):
-            pass
-        try:
-            self._p.wait(timeout=60)
-        except subprocess.TimeoutExpired:
-            self._p.kill()
-            self._p.wait()
-        self._p = None
+        self.barrier()
+        self._open = False
+        self._post(f"left.{self.rank}", None)
+        if self.rank == 0:  # every rank has passed the last barrier and said so
+            self._wait([os.path.join(self.path, f"left.{r}") for r in range(self.world)])
+            shutil.rmtree(self.path, ignore_errors=True)
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
         self.close()
-
-
-def _serve(timeout_s: float):
-    """Sidecar: join the gloo group as $RANK and answer requests on stdin."""
-    # replies go to the original stdout; anything torch / gloo print (gloo
-    # logs "[Gloo] Rank 0 is connected ..." to stdout) goes to stderr
-    out = os.fdopen(os.dup(1), "w")
-    os.dup2(2, 1)
-    sys.stdout = sys.stderr
-    import datetime
-    import torch
-    import torch.distributed as dist
-
-    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=timeout_s))
-    rank, world = dist.get_rank(), dist.get_world_size()
-    for line in sys.stdin:
-        req = json.loads(line)
-        op, value = req["op"], req.get("value")
-        try:
-            if op == "ready":
-                res = None
-            elif op == "bcast":
-                box = [value]
-                dist.broadcast_object_list(box, src=0)
-                res = box[0]
-            elif op == "barrier":
-                dist.barrier()
-                res = None
-            elif op == "max":
-                t = torch.tensor([value], dtype=torch.float64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                res = t.item()
-            elif op == "gather":
-                box = [None] * world
-                dist.all_gather_object(box, value)
-                res = box
-            elif op == "close":
-                out.write(json.dumps({"value": None}) + "\n")
-                out.flush()
-                break
-            else:
-                raise ValueError(f"unknown op {op!r}")
-            out.write(json.dumps({"value": res}) + "\n")
-        except Exception as e:  # report to the GPU process, which raises
-            out.write(json.dumps({"error": f"rank {rank}: {e!r}"}) + "\n")
-        out.flush()
-    dist.destroy_process_group()
-
-
-if __name__ == "__main__":
-    _serve(float(sys.argv[1]) if len(sys.argv) > 1 else 600.0)

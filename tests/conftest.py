@@ -18,7 +18,7 @@ U64 = (1 << 64) - 1
 def pytest_configure(config):
     # libbtcminer.so binds to /opt/rocm's HIP runtime; torch bundles its own.
     # Keep torch out of this process so only one runtime is mapped (bench.py
-    # does the same: torch.distributed runs in a rendezvous sidecar process).
+    # does the same: its ranks meet over a file rendezvous, not torch).
     config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) GPU")
     config.addinivalue_line("markers", "slow: long-running CPU test")
 

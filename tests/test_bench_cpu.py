@@ -68,7 +68,7 @@ def test_multi_gpu_without_devices_fails_loudly():
 
 def test_bench_imports_no_torch():
     """The bench process itself never imports torch (torch.distributed runs in
-    the rendezvous sidecar), so it maps one HIP runtime."""
+    a file rendezvous), so it maps one HIP runtime."""
     import ast
     tree = ast.parse(open(os.path.join(ROOT, "bench.py")).read())
     mods = {a.name.split(".")[0] for n in ast.walk(tree) if isinstance(n, ast.Import) for a in n.names}

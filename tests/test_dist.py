@@ -1,12 +1,9 @@
 """Multi-rank sharding on CPU: the range split (dist.split_range, the mirror of
 bm::split_range), the lexicographic combine, and the torchrun-style
-rendezvous (distributed_bitcoin_minter_amd/rendezvous.py: torch.distributed
-gloo in a sidecar process) at world sizes 2 and 4.  On CPU each rank's scan
-is the oracle; the same workers run the HIP search in the -m gpu variant
-(every rank on GPU 0), so no N>1 test is left without the real kernels.
-
-torch is imported only inside the sidecars: the pytest process keeps a
-single HIP runtime (/opt/rocm's) for the GPU tests."""
+rendezvous (distributed_bitcoin_minter_amd/rendezvous.py: files on the node,
+no torch) at world sizes 2, 4 and 8.  On CPU each rank's scan is the oracle;
+the same workers run the HIP search in the -m gpu variant (every rank on
+GPU 0), so no N>1 test is left without the real kernels."""
 import json
 import os
 import random
@@ -53,7 +50,7 @@ def _free_port():
     return port
 
 
-# One rank: rendezvous (gloo sidecar), a broadcast of rank 0's bytes (the
+# One rank: rendezvous (node files), a broadcast of rank 0's bytes (the
 # RCCL unique id's path), its piece scanned (oracle on CPU, HIP on GPU),
 # gather + lexicographic min, max over ranks.
 _RANK = r"""
@@ -105,7 +102,7 @@ def _check(outs, world, want, lo, hi):
     assert pieces == split_range(lo, hi, world)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_rendezvous_combine_equals_single_scan(oracle, world):
     msg, lo, hi = b"bradfitz", 0, 99_999
     _check(_run_ranks(world, "cpu", msg, lo, hi), world, oracle.search(msg, lo, hi), lo, hi)

@@ -228,7 +228,7 @@ def test_bench_one_process_rehearsal():
 
 
 def test_bench_torchrun_rehearsal():
-    """bench.py under torchrun with 2 ranks on GPU 0 (gloo sidecar rendezvous,
+    """bench.py under torchrun with 2 ranks on GPU 0 (file rendezvous,
     gather of the partials); the GPU processes map one HIP runtime."""
     out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--rehearse-one-gpu"], torchrun=2))
     assert out["n_gpus"] == 2 and out["result_ok"] in (True, None)
