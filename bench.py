@@ -275,6 +275,10 @@ def open_contexts(args, world, rank, local):
     """(ctx, group, search, parallelism) for the launch mode (module docstring)."""
     if world > 1:
         from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
+        if not args.rehearse_one_gpu and local >= device_count():
+            log(f"error: LOCAL_RANK {local} but only {device_count()} HIP device(s) visible "
+                "(--rehearse-one-gpu runs every rank on GPU 0)")
+            sys.exit(2)
         grp = Group(Rendezvous())
         if args.rehearse_one_gpu or args.combine == "gather":
             # every rank scans its piece on its own context; the 16-byte
