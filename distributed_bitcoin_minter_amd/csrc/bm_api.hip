@@ -783,7 +783,8 @@ int bm_reduce_gpu(bm_ctx_t* ctx, const bm_result_t* parts, size_t n, bm_result_t
 }
 
 int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches) {
-    if (!ctx || launches < -1) return BM_EINVAL;
+    // not for rank contexts: a rank failing alone would leave the others in the allgather
+    if (!ctx || launches < -1 || (ctx->world > 1 && launches >= 0)) return BM_EINVAL;
     ctx->fault_after = launches;
     return BM_OK;
 }

@@ -185,7 +185,9 @@ int bm_reduce_gpu(bm_ctx_t* ctx, const bm_result_t* parts, size_t n, bm_result_t
 
 /* Make every later bm_search_gpu fail with BM_EINTERNAL after enqueueing
  * `launches` search launches (-1: off).  Exercises the failure path: the
- * call drains what it queued and the context stays usable. */
+ * call drains what it queued and the context stays usable.  BM_EINVAL on a
+ * rank context of more than one rank (one rank failing alone would leave the
+ * others waiting in the allgather). */
 int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches);
 
 /* ---- host-side plan introspection (pure CPU; used by the CPU tests) ---- */
