@@ -422,8 +422,10 @@ def main():
                 "unit": "T int32 lane-ops/s", "frac": round(achieved / VALU_PEAK_T, 4),
                 "traffic": pmc.get("hbm_bytes_per_launch"),
                 "traffic_unit": "memory-side bytes per launch (PMC FETCH_SIZE+WRITE_SIZE)",
-                "traffic_note": "the per-launch dequeue counter's returning atomics; the search reads no input "
-                                "from HBM (DESIGN.md §5)",
+                "traffic_note": "memory-side writes of the dequeue counter's returning atomics and of the rare "
+                                "path's spilled best (hash, nonce); the search reads no input from HBM "
+                                "(DESIGN.md §5, §8). FETCH_SIZE is not doubled: the guide's x2 is for 16-B/lane "
+                                "streaming reads, which this kernel does not issue",
                 "pmc_src": pmc_src,
                 "kernel": f"search_kernel<P={dom.p},NBV={dom.nbv}> ({dom.digits}-digit nonces)",
                 "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom.nonces,

@@ -122,3 +122,41 @@ def test_rendezvous_ranks_on_gpu(oracle, world):
     across the 9->10 digit boundary, split over the ranks."""
     msg, lo, hi = b"bradfitz", 999_000_000, 1_000_999_999
     _check(_run_ranks(world, "gpu", msg, lo, hi), world, oracle.search(msg, lo, hi, threads=8), lo, hi)
+
+
+def _gloo_worker(rank, world, port, msg, lo, hi, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    from conftest import Oracle
+    from distributed_bitcoin_minter_amd.dist import combine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    oracle = Oracle(os.path.join(ROOT, "oracle", "liboracle.so"))
+    piece = rank_piece(lo, hi, rank, world)
+    part = oracle.search(msg, *piece) if piece else (U64, U64)
+    q.put((rank, combine(part)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_torch_gloo_combine_equals_single_scan(oracle, world):
+    """dist.combine, the torch.distributed form of the combine (one
+    all_gather_into_tensor of 2 x u64 per rank; RCCL under the "nccl" backend,
+    tests/test_dist_gpu.py), over gloo at world sizes 2 and 4, with the oracle
+    as each rank's scan: the lexicographic min equals one scan of the range,
+    including partials >= 2^63 (two's-complement transport)."""
+    import multiprocessing as mp
+    for msg, lo, hi in ((b"bradfitz", 0, 99_999), (b"bradfitz", U64 - 5000, U64)):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, msg, lo, hi, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        out = [q.get(timeout=120) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        assert all(res == oracle.search(msg, lo, hi) for _, res in out), out
