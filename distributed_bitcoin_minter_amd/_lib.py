@@ -20,7 +20,7 @@ BM_ENOMEM = -5
 BM_EINTERNAL = -6
 BM_MAX_LAUNCH_STATS = 64
 BM_RCCL_ID_BYTES = 128
-BM_ABI_VERSION = 2
+BM_ABI_VERSION = 3
 BM_COMBINE_AUTO, BM_COMBINE_RCCL, BM_COMBINE_HOST = 0, 1, 2
 U64_MAX = (1 << 64) - 1
 
@@ -106,7 +106,9 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
-    if lib.bm_abi_version() != BM_ABI_VERSION:
+    # an explicit BTCMINER_LIB (A/B of older builds, tools/ab_bench.py) may
+    # predate the current stats layout; the in-tree library must match
+    if lib.bm_abi_version() != BM_ABI_VERSION and not os.environ.get("BTCMINER_LIB"):
         raise OSError(f"{LIB_PATH}: ABI version {lib.bm_abi_version()}, expected {BM_ABI_VERSION}; rebuild it")
     _lib = lib
     return lib

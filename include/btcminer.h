@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BM_ABI_VERSION 2
+#define BM_ABI_VERSION 3
 
 /* status codes */
 #define BM_OK 0

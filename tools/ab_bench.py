@@ -39,7 +39,7 @@ def one(reps):
             n = c["upper"] - c["lower"] + 1
             dom = best[2][0]
             out[cfg] = {"wall_ms": round(best[0], 3), "GHs": round(n / best[0] / 1e6, 3),
-                        "dom_GHs": round(dom[0] / dom[1] / 1e6, 3), "dom": dom,
+                        "dom_GHs": round(dom[0] / dom[1] / 1e6, 3) if dom[1] > 0 else None, "dom": dom,
                         "top": best[2]}
     print(json.dumps(out), flush=True)
 
