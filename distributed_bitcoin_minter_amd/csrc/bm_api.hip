@@ -106,8 +106,6 @@ struct bm_ctx {
     int rank = 0, world = 1;  // bm_ctx_create_rank: this process's place in an RCCL process group
     int fault_after = -1;     // test hook: fail after enqueueing this many launches (-1: off)
     uint64_t lane_chunk = bm::kNoncesPerLaneChunk;  // nonces per lane per dequeue, at most (BTCMINER_CHUNK)
-    int guided = 0;              // guided dequeue divisor K (BTCMINER_GUIDED; 0: fixed chunks)
-    uint64_t guided_cap = 1600;  // guided: nonces per lane per dequeue, at most (BTCMINER_GUIDED_CAP)
     bm_stats_t stats;
 };
 
@@ -158,17 +156,6 @@ int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_
     const uint64_t m_max = std::max<uint64_t>(1, ctx->lane_chunk / S);
     const uint32_t m = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>(m_max, T / (8 * resident * (uint64_t)kBlock)));
-    // Guided dequeue (BTCMINER_GUIDED = K > 0): a wave takes
-    // remaining / (K * resident lanes) tasks per lane (a power-of-two divisor),
-    // at most guided_cap nonces per lane, at least one task: few atomics while
-    // much is left, the same one-task drain at the end.  The grid is sized
-    // from the fixed chunks as before.
-    uint32_t guide_shift = 0, chunk_m = m;
-    if (ctx->guided > 0) {
-        const uint64_t div = (uint64_t)ctx->guided * resident * (uint64_t)kBlock;
-        while ((1ull << (guide_shift + 1)) <= div) ++guide_shift;
-        chunk_m = (uint32_t)std::max<uint64_t>(1, ctx->guided_cap / S);
-    }
     const uint64_t chunks = (T + 64ull * m - 1) / (64ull * m);
     const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, resident));
     const uint64_t k = (chunks + grid * 4 - 1) / (grid * 4);  // chunks per wave (approx.)
@@ -188,12 +175,11 @@ int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_
     A.nonce_base = s.nonce_base;
     A.t0 = t0;
     A.t_end = t_end;
-    A.chunk_m = chunk_m;
+    A.chunk_m = m;
     A.S = (uint32_t)S;
     A.ms = (uint32_t)ms;
     A.nd = (uint32_t)s.nd;
     A.part_off = part_off;
-    A.guide_shift = guide_shift;
     L.fn = fn;
     L.grid = (uint32_t)grid;
     std::memset(&L.stat, 0, sizeof L.stat);
@@ -656,14 +642,7 @@ void read_env(bm_ctx* ctx) {
         const unsigned long long v = std::strtoull(e, &end, 10);
         if (end != e && *end == '\0' && errno == 0 && v >= 10 && v <= 100000) ctx->lane_chunk = v;
     }
-    if (const char* e = std::getenv("BTCMINER_GUIDED")) {
-        const int v = std::atoi(e);
-        if (v >= 0 && v <= 64) ctx->guided = v;
-    }
-    if (const char* e = std::getenv("BTCMINER_GUIDED_CAP")) {
-        const long long v = std::atoll(e);
-        if (v >= 10 && v <= 100000) ctx->guided_cap = (uint64_t)v;
-    }
+
 }
 
 int create_ctx(const int* devices, int n, int nslots, bm_ctx** out) {

@@ -25,8 +25,7 @@ struct SearchArgs {
     uint32_t ms;         // digits iterated by the inner loop (all in one word)
     uint32_t nd;         // digits of v placed in the varying block(s)
     uint32_t part_off;   // first partial slot written by this launch
-    uint32_t guide_shift;  // 0: every dequeue takes chunk_m tasks per lane; else guided:
-                           // min(chunk_m, max(1, remaining >> guide_shift)) tasks per lane
+    uint32_t pad_;
 };
 
 struct HashArgs {

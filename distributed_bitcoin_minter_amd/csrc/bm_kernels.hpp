@@ -391,21 +391,12 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
         counter[kClockSlot + 0] = __builtin_amdgcn_s_memtime();
         counter[kClockSlot + 1] = __builtin_amdgcn_s_memrealtime();
     }
-    uint64_t rem = ntask;  // tasks left as of this wave's last dequeue (guided sizing)
     for (;;) {
-        // guided: big chunks while much is left, one task per lane at the end
-        // (fewer returning atomics, the same fine drain); wave-uniform
-        uint32_t m = A.chunk_m;
-        if (A.guide_shift) {
-            const uint64_t g = rem >> A.guide_shift;
-            m = (uint32_t)(g < 1 ? 1 : (g < (uint64_t)A.chunk_m ? g : A.chunk_m));
-        }
         uint64_t base = 0;
-        if (lane == 0) base = atomicAdd(counter, (unsigned long long)(A.guide_shift ? 64ull * m : chunk));
+        if (lane == 0) base = atomicAdd(counter, (unsigned long long)chunk);
         base = readfirstlane_u64(base);
         if (base >= ntask) break;
-        rem = ntask - base;
-        for (uint32_t i = 0; i < m; ++i) {
+        for (uint32_t i = 0; i < A.chunk_m; ++i) {
             const uint64_t tt = base + 64ull * i + lane;
             if (tt >= ntask) break;
             const uint64_t t = A.t0 + tt;
