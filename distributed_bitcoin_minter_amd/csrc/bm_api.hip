@@ -351,7 +351,7 @@ int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches,
         // nparts = 0 (a device or rank with nothing to scan) writes (2^64-1, 2^64-1)
         reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, d.d_result);
         BM_HIP(hipGetLastError());
-        if (ctx->timing && !launches[di].empty())  // the clock stamps, for the launch statistics
+        if (BM_CLOCK_PROBE && ctx->timing && !launches[di].empty())  // clock stamps, for the launch stats
             BM_HIP(hipMemcpyAsync(d.h_ctr, d.d_ctr, launches[di].size() * kCtrStride * sizeof(unsigned long long),
                                   hipMemcpyDeviceToHost, d.stream));
     }
@@ -495,7 +495,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
                 L.stat.ms = ms;
                 st.kernel_ms += ms;
                 const unsigned long long* c = d.h_ctr + kCtrStride * li + kClockSlot - 1;
-                if (c[4] > c[2] && c[3] > c[1])  // shader cycles over constant-rate ticks
+                if (BM_CLOCK_PROBE && c[4] > c[2] && c[3] > c[1])  // shader cycles over constant-rate ticks
                     L.stat.clock_ghz = (double)(c[3] - c[1]) / ((double)(c[4] - c[2]) / d.wall_clock_hz) / 1e9;
                 if (span_ok) {  // the first launch's start to this launch's end
                     float sp = 0.f;
