@@ -18,16 +18,28 @@ from conftest import ROOT, U64
 from distributed_bitcoin_minter_amd.bitcoin import Message, MsgType, NewJoin, NewRequest, NewResult
 
 EXE = os.path.join(ROOT, "examples", "bm_miner")
+CLIENT = os.path.join(ROOT, "examples", "bm_client")
+_HDRS = [os.path.join(ROOT, "include", h) for h in ("btcminer.hpp", "btcminer.h", "bm_json.hpp", "lsp.hpp")]
+
+
+def _build(exe, src, gpu_lib):
+    """(Re)build an example when it is older than its sources (the same
+    command line as __graft_entry__.build)."""
+    if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(p) for p in [src] + _HDRS):
+        cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-pthread", "-I", os.path.join(ROOT, "include"), src]
+        if gpu_lib:
+            cmd += ["-L", os.path.join(ROOT, "distributed_bitcoin_minter_amd"), "-lbtcminer",
+                    "-Wl,-rpath,$ORIGIN/../distributed_bitcoin_minter_amd"]
+        subprocess.check_call(cmd + ["-o", exe])
+    return exe
 
 
 def _exe():
-    src = [os.path.join(ROOT, "examples", "bm_miner.cpp"), os.path.join(ROOT, "include", "btcminer.hpp"),
-           os.path.join(ROOT, "include", "btcminer.h")]
-    if not os.path.exists(EXE) or os.path.getmtime(EXE) < max(os.path.getmtime(p) for p in src):
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-                               src[0], "-L", os.path.join(ROOT, "distributed_bitcoin_minter_amd"), "-lbtcminer",
-                               "-Wl,-rpath,$ORIGIN/../distributed_bitcoin_minter_amd", "-o", EXE])
-    return EXE
+    return _build(EXE, os.path.join(ROOT, "examples", "bm_miner.cpp"), True)
+
+
+def _client():
+    return _build(CLIENT, os.path.join(ROOT, "examples", "bm_client.cpp"), False)
 
 
 def _selftest(lines):
@@ -84,7 +96,7 @@ def test_miner_without_gpu_fails_loudly():
     from distributed_bitcoin_minter_amd import device_count
     if device_count() > 0:
         pytest.skip("a GPU is present")
-    r = subprocess.run([_exe()], input=NewRequest("bradfitz", 0, 9999).marshal() + b"\n", capture_output=True,
+    r = subprocess.run([_exe(), "--stdin"], input=NewRequest("bradfitz", 0, 9999).marshal() + b"\n", capture_output=True,
                        timeout=60)
     assert r.returncode == 2 and r.stdout.startswith(b"error -2 ")
 
@@ -97,7 +109,7 @@ def test_miner_job_loop_on_gpu(oracle):
             1_000_020_000), ("bradfitz", U64 - 3000, U64), ("x", 10, 9)]
     lines = [NewRequest(*q).marshal() for q in reqs[:2]] + [NewJoin().marshal(), b"garbage", NewResult(1, 2).marshal()]
     lines += [NewRequest(*q).marshal() for q in reqs[2:]]
-    r = subprocess.run([_exe()], input=b"".join(l + b"\n" for l in lines), capture_output=True, timeout=120)
+    r = subprocess.run([_exe(), "--stdin"], input=b"".join(l + b"\n" for l in lines), capture_output=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     out = r.stdout.split(b"\n")
     assert out[0] == NewJoin().marshal()
@@ -105,6 +117,6 @@ def test_miner_job_loop_on_gpu(oracle):
     assert [Message.unmarshal(o) for o in out[1:1 + len(reqs)]] == [NewResult(h, n) for h, n in want]
     assert b"bad job" in r.stderr
     # miner.go:59's exclusive upper
-    r = subprocess.run([_exe(), "--exclusive-upper"], input=NewRequest("bradfitz", 0, 10000).marshal() + b"\n",
+    r = subprocess.run([_exe(), "--stdin", "--exclusive-upper"], input=NewRequest("bradfitz", 0, 10000).marshal() + b"\n",
                        capture_output=True, timeout=60)
     assert Message.unmarshal(r.stdout.split(b"\n")[1]) == NewResult(*oracle.search_excl(b"bradfitz", 0, 10000))
