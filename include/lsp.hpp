@@ -1,14 +1,15 @@
-// lsp.hpp -- C++17 client side of the Live Sequence Protocol, the transport the
-// reference's miner and request client speak (project2/README.md:67-239).
+// lsp.hpp -- C++17 Live Sequence Protocol, the transport the reference's
+// server, miners and request clients speak (project2/README.md:67-239).
 //
-// It is the C++ twin of distributed_bitcoin_minter_amd/lsp.py's client and
-// talks to that server (or to any conforming one) over UDP:
+// It is the C++ twin of distributed_bitcoin_minter_amd/lsp.py and interoperates
+// with it (or any conforming endpoint) over UDP:
 //
 //   lsp::Params           params.go:8-35 (EpochLimit 5, EpochMillis 2000, WindowSize 1)
 //   lsp::Message          message.go:10-66, marshalled as Go's encoding/json does
 //                         ({"Type":..,"ConnID":..,"SeqNum":..,"Payload":base64|null})
 //   lsp::Client           client_api.go:6-30: NewClient / ConnID / Read / Write / Close
-//   lspnet::Set...DropPercent   staff.go:31-43, the client-side drop injection
+//   lsp::Server           server_api.go:6-39: NewServer / Read / Write / CloseConn / Close
+//   lspnet::Set...DropPercent   staff.go:15-63, per-role drop injection
 //
 // Protocol rules (README:67-138), as in lsp.py:
 //   * connect: (Connect,0,0) every epoch until (Ack,id,0); K epochs -> error;
@@ -18,12 +19,16 @@
 //   * each epoch: Ack 0 while no data has arrived, resend unacked data, re-ack
 //     the last WindowSize distinct data seqnums; K silent epochs -> lost;
 //   * Close blocks until everything written is acknowledged or the
-//     connection is lost.
-// One background thread per client reads the socket and runs the epoch timer;
-// all state sits behind one mutex.
+//     connection is lost;
+//   * the server numbers connections from 1 and answers a repeated Connect
+//     from the same address with the same id.
+// One background thread per endpoint reads the socket and runs the epoch
+// timer; all state sits behind one mutex.
 #pragma once
 
+#include <arpa/inet.h>
 #include <netdb.h>
+#include <netinet/in.h>
 #include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -34,6 +39,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -49,35 +55,42 @@
 
 namespace lspnet {
 
-// staff.go:15-63: package-global drop percentages (0..100) of this process's
-// client reads and writes.
+// staff.go:15-63: package-global drop percentages (0..100) per role
+// (a Client's socket is a client, a Server's a server) and direction.
 namespace detail {
-inline std::atomic<int>& read_drop() {
-    static std::atomic<int> v{0};
-    return v;
+enum Knob { kClientRead, kClientWrite, kServerRead, kServerWrite };
+inline std::atomic<int>& knob(Knob k) {
+    static std::atomic<int> v[4] = {{0}, {0}, {0}, {0}};
+    return v[k];
 }
-inline std::atomic<int>& write_drop() {
-    static std::atomic<int> v{0};
-    return v;
-}
-inline bool drop(int pct) {
+inline bool drop(Knob k) {  // conn.go:115-117
+    const int pct = knob(k);
     if (pct <= 0) return false;
     static std::mutex mu;
     static std::mt19937 rng{std::random_device{}()};
     std::lock_guard<std::mutex> g(mu);
     return (int)(rng() % 100) < pct;
 }
+inline void set(Knob k, int p) {
+    if (p >= 0 && p <= 100) knob(k) = p;
+}
 }  // namespace detail
 
-inline void SetClientReadDropPercent(int p) {
-    if (p >= 0 && p <= 100) detail::read_drop() = p;
+inline void SetClientReadDropPercent(int p) { detail::set(detail::kClientRead, p); }
+inline void SetClientWriteDropPercent(int p) { detail::set(detail::kClientWrite, p); }
+inline void SetServerReadDropPercent(int p) { detail::set(detail::kServerRead, p); }
+inline void SetServerWriteDropPercent(int p) { detail::set(detail::kServerWrite, p); }
+inline void SetReadDropPercent(int p) {
+    SetClientReadDropPercent(p);
+    SetServerReadDropPercent(p);
 }
-inline void SetClientWriteDropPercent(int p) {
-    if (p >= 0 && p <= 100) detail::write_drop() = p;
+inline void SetWriteDropPercent(int p) {
+    SetClientWriteDropPercent(p);
+    SetServerWriteDropPercent(p);
 }
 inline void ResetDropPercent() {
-    SetClientReadDropPercent(0);
-    SetClientWriteDropPercent(0);
+    SetReadDropPercent(0);
+    SetWriteDropPercent(0);
 }
 
 constexpr size_t kMaxPacket = 2000;  // conn.go:35
@@ -225,95 +238,252 @@ inline Message NewData(int64_t connID, int64_t seqNum, std::string payload) {
 }
 inline Message NewAck(int64_t connID, int64_t seqNum) { return Message{MsgType::Ack, connID, seqNum, std::nullopt}; }
 
+
 namespace detail {
 
-// A UDP socket connected to host:port (lspnet.Dial); drops per lspnet.
-class Conn {
+// A UDP socket in one lspnet role: a client's is connected to its server, a
+// server's is bound to a port.  Reads and writes are dropped per lspnet.
+class Socket {
    public:
-    explicit Conn(const std::string& hostport) {
+    static std::unique_ptr<Socket> dial(const std::string& hostport) {  // net.go:58-76
         const size_t colon = hostport.rfind(':');
         if (colon == std::string::npos) throw LSPError("bad address " + hostport);
-        const std::string host = hostport.substr(0, colon), port = hostport.substr(colon + 1);
+        std::string host = hostport.substr(0, colon);
+        const std::string port = hostport.substr(colon + 1);
+        if (host.empty() || host == "localhost") host = "127.0.0.1";
         addrinfo hints{}, *res = nullptr;
         hints.ai_family = AF_UNSPEC;
         hints.ai_socktype = SOCK_DGRAM;
         if (getaddrinfo(host.c_str(), port.c_str(), &hints, &res) != 0 || !res)
             throw LSPError("cannot resolve " + hostport);
+        int fd = -1;
         for (addrinfo* a = res; a; a = a->ai_next) {
-            fd_ = ::socket(a->ai_family, a->ai_socktype, a->ai_protocol);
-            if (fd_ < 0) continue;
-            if (::connect(fd_, a->ai_addr, a->ai_addrlen) == 0) break;
-            ::close(fd_);
-            fd_ = -1;
+            fd = ::socket(a->ai_family, a->ai_socktype, a->ai_protocol);
+            if (fd < 0) continue;
+            if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) break;
+            ::close(fd);
+            fd = -1;
         }
         freeaddrinfo(res);
-        if (fd_ < 0) throw LSPError("cannot reach " + hostport);
+        if (fd < 0) throw LSPError("cannot reach " + hostport);
+        return std::unique_ptr<Socket>(new Socket(fd, false));
     }
-    ~Conn() {
-        if (fd_ >= 0) ::close(fd_);
+    static std::unique_ptr<Socket> listen(int port, const std::string& host) {  // net.go:37-52
+        const int fd = ::socket(AF_INET, SOCK_DGRAM, 0);
+        if (fd < 0) throw LSPError("cannot open a UDP socket");
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_port = htons((uint16_t)port);
+        if (port < 0 || port > 65535 || inet_pton(AF_INET, host.c_str(), &a.sin_addr) != 1 ||
+            ::bind(fd, (sockaddr*)&a, sizeof a) != 0) {
+            ::close(fd);
+            throw LSPError("cannot listen on " + host + ":" + std::to_string(port));
+        }
+        return std::unique_ptr<Socket>(new Socket(fd, true));
     }
-    Conn(const Conn&) = delete;
-    Conn& operator=(const Conn&) = delete;
+    ~Socket() { ::close(fd_); }
+    Socket(const Socket&) = delete;
+    Socket& operator=(const Socket&) = delete;
 
-    void write(const std::string& b) {
-        if (lspnet::detail::drop(lspnet::detail::write_drop())) return;
-        (void)::send(fd_, b.data(), b.size(), 0);  // UDP: a failed send is a lost packet
+    int local_port() const {
+        sockaddr_storage a{};
+        socklen_t n = sizeof a;
+        getsockname(fd_, (sockaddr*)&a, &n);
+        return ntohs(a.ss_family == AF_INET6 ? ((sockaddr_in6*)&a)->sin6_port : ((sockaddr_in*)&a)->sin_port);
     }
-    // One datagram, or nullopt after timeout_ms (or a dropped read).
-    std::optional<std::string> read(int timeout_ms) {
+    // to = empty: the connected peer; else a peer address from read()
+    void write(const std::string& b, const std::string& to = {}) {
+        if (lspnet::detail::drop(server_ ? lspnet::detail::kServerWrite : lspnet::detail::kClientWrite)) return;
+        if (to.empty()) (void)::send(fd_, b.data(), b.size(), 0);  // UDP: a failed send is a lost packet
+        else (void)::sendto(fd_, b.data(), b.size(), 0, (const sockaddr*)to.data(), (socklen_t)to.size());
+    }
+    // One datagram and its sender's address, or nullopt after timeout_ms (or
+    // a dropped read).
+    std::optional<std::pair<std::string, std::string>> read(int timeout_ms) {
         pollfd p{fd_, POLLIN, 0};
         if (::poll(&p, 1, timeout_ms) <= 0) return std::nullopt;
         char buf[lspnet::kMaxPacket];
-        const ssize_t n = ::recv(fd_, buf, sizeof buf, 0);
+        sockaddr_storage from{};
+        socklen_t flen = sizeof from;
+        const ssize_t n = ::recvfrom(fd_, buf, sizeof buf, 0, (sockaddr*)&from, &flen);
         if (n < 0) return std::nullopt;
-        if (lspnet::detail::drop(lspnet::detail::read_drop())) return std::nullopt;
-        return std::string(buf, (size_t)n);
+        if (lspnet::detail::drop(server_ ? lspnet::detail::kServerRead : lspnet::detail::kClientRead))
+            return std::nullopt;
+        return std::make_pair(std::string(buf, (size_t)n), std::string((const char*)&from, flen));
     }
 
    private:
-    int fd_ = -1;
+    Socket(int fd, bool server) : fd_(fd), server_(server) {}
+    int fd_;
+    bool server_;
 };
+
+// Protocol state of one end of one connection, no I/O of its own (lsp.py's
+// _Endpoint).  The owner holds its lock around every call.
+class Endpoint {
+   public:
+    Endpoint(int64_t id, const Params& p, std::function<void(const Message&)> send)
+        : id_(id), w_(std::max(1, p.WindowSize)), k_(std::max(1, p.EpochLimit)), send_(std::move(send)) {}
+
+    int64_t id() const { return id_; }
+    bool lost() const { return lost_; }
+    bool drained() const { return pending_.empty() && unacked_.empty(); }
+
+    void write(std::string payload) {
+        pending_.push_back(std::move(payload));
+        pump();
+    }
+    // One received message; appends the payloads now deliverable to `out`.
+    void on_message(const Message& m, std::deque<std::string>& out) {
+        idle_ = 0;
+        if (m.Type == MsgType::Ack) {
+            if (unacked_.erase(m.SeqNum)) pump();
+            return;
+        }
+        if (m.Type != MsgType::Data || m.SeqNum < 1) return;
+        const int64_t s = m.SeqNum;
+        if (s >= expect_ + w_) return;  // beyond the receive window: the sender cannot be there, discard
+        send_(NewAck(id_, s));
+        if (std::find(recent_.begin(), recent_.end(), s) == recent_.end()) {
+            recent_.push_back(s);
+            if ((int)recent_.size() > w_) recent_.pop_front();
+        }
+        got_data_ = true;
+        if (s >= expect_) ooo_.emplace(s, m.Payload.value_or(""));
+        for (auto it = ooo_.find(expect_); it != ooo_.end(); it = ooo_.find(expect_)) {
+            out.push_back(std::move(it->second));
+            ooo_.erase(it);
+            ++expect_;
+        }
+    }
+    // One epoch; true when the connection is (now) lost.
+    bool on_epoch() {
+        if (lost_) return true;
+        if (++idle_ >= k_) return lost_ = true;
+        if (!got_data_) send_(NewAck(id_, 0));
+        for (const auto& kv : unacked_) send_(kv.second);
+        for (int64_t s : recent_) send_(NewAck(id_, s));
+        return false;
+    }
+
+   private:
+    bool window_open() const {
+        const int64_t base = unacked_.empty() ? next_seq_ : unacked_.begin()->first;
+        return next_seq_ < base + w_;
+    }
+    void pump() {
+        while (!pending_.empty() && window_open()) {
+            Message m = NewData(id_, next_seq_, std::move(pending_.front()));
+            pending_.pop_front();
+            unacked_.emplace(next_seq_++, m);
+            send_(m);
+        }
+    }
+
+    const int64_t id_;
+    const int w_, k_;
+    std::function<void(const Message&)> send_;
+    int64_t next_seq_ = 1, expect_ = 1;  // next outgoing / next in-order incoming seqnum
+    std::deque<std::string> pending_;    // waiting for the window
+    std::map<int64_t, Message> unacked_;  // sent, not acknowledged
+    std::map<int64_t, std::string> ooo_;  // received ahead of expect_
+    std::deque<int64_t> recent_;          // last w distinct data seqnums received
+    bool got_data_ = false, lost_ = false;
+    int idle_ = 0;  // epochs since anything was received
+};
+
+// The background thread of an endpoint: socket reads (50 ms polls) and the
+// epoch timer, until stop() is called.
+class Pump {
+   public:
+    using clock = std::chrono::steady_clock;
+    Pump(Socket& sock, int epoch_ms, std::mutex& mu, std::function<void()> on_epoch,
+         std::function<void(std::string, std::string)> on_packet)
+        : sock_(sock), period_(epoch_ms), mu_(mu), on_epoch_(std::move(on_epoch)), on_packet_(std::move(on_packet)) {
+        thread_ = std::thread([this] { loop(); });
+    }
+    ~Pump() { stop(); }
+    void stop() {  // caller must not hold the lock
+        stop_ = true;
+        if (thread_.joinable()) thread_.join();
+    }
+
+   private:
+    void loop() {
+        auto next = clock::now() + period_;
+        while (!stop_) {
+            if (clock::now() >= next) {
+                next += period_;
+                std::lock_guard<std::mutex> g(mu_);
+                on_epoch_();
+            }
+            const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(next - clock::now()).count();
+            auto got = sock_.read((int)std::clamp<long long>(left, 0, 50));
+            if (!got) continue;
+            std::lock_guard<std::mutex> g(mu_);
+            on_packet_(std::move(got->first), std::move(got->second));
+        }
+    }
+    Socket& sock_;
+    const std::chrono::milliseconds period_;
+    std::mutex& mu_;
+    std::function<void()> on_epoch_;
+    std::function<void(std::string, std::string)> on_packet_;
+    std::atomic<bool> stop_{false};
+    std::thread thread_;
+};
+
+inline std::optional<Message> parse(const std::string& raw) {
+    try {
+        return Message::Unmarshal(raw);
+    } catch (const bmjson::DecodeError&) {
+        return std::nullopt;  // a stray datagram
+    }
+}
 
 }  // namespace detail
 
 // client_api.go:6-30.  Create with NewClient.
 class Client {
    public:
-    Client(std::unique_ptr<detail::Conn> conn, int64_t id, const Params& p)
-        : conn_(std::move(conn)), p_(p), id_(id), w_(std::max(1, p.WindowSize)), k_(std::max(1, p.EpochLimit)) {
-        thread_ = std::thread([this] { loop(); });
+    Client(std::unique_ptr<detail::Socket> sock, int64_t id, const Params& p)
+        : sock_(std::move(sock)), ep_(id, p, [this](const Message& m) { sock_->write(m.Marshal()); }) {
+        pump_ = std::make_unique<detail::Pump>(
+            *sock_, p.EpochMillis, mu_,
+            [this] {
+                if (ep_.on_epoch()) cv_.notify_all();
+            },
+            [this](std::string raw, std::string) {
+                const auto m = detail::parse(raw);
+                if (!m || m->ConnID != ep_.id() || ep_.lost()) return;
+                const size_t before = reads_.size();
+                ep_.on_message(*m, reads_);
+                if (reads_.size() != before || ep_.drained()) cv_.notify_all();
+            });
     }
     Client(const Client&) = delete;
     Client& operator=(const Client&) = delete;
-    ~Client() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        if (thread_.joinable()) thread_.join();
-    }
+    ~Client() { pump_->stop(); }
 
-    int64_t ConnID() const { return id_; }
+    int64_t ConnID() const { return ep_.id(); }
 
     // Blocks for the next payload; LSPError once closed or lost with nothing left.
     std::string Read() {
         std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return !reads_.empty() || lost_ || closing_; });
+        cv_.wait(g, [&] { return !reads_.empty() || ep_.lost() || closing_; });
         if (!reads_.empty()) {
             std::string r = std::move(reads_.front());
             reads_.pop_front();
             return r;
         }
-        throw LSPError(lost_ ? "connection lost" : "connection closed");
+        throw LSPError(ep_.lost() ? "connection lost" : "connection closed");
     }
 
     // Non-blocking; LSPError only if the connection has been lost.
     void Write(std::string payload) {
         std::lock_guard<std::mutex> g(mu_);
-        if (lost_) throw LSPError("connection lost");
-        pending_.push_back(std::move(payload));
-        pump();
+        if (ep_.lost()) throw LSPError("connection lost");
+        ep_.write(std::move(payload));
     }
 
     // Blocks until every written message is acknowledged (or the connection
@@ -324,135 +494,203 @@ class Client {
             std::unique_lock<std::mutex> g(mu_);
             closing_ = true;
             cv_.notify_all();
-            cv_.wait(g, [&] { return drained() || lost_; });
-            lost_pending = lost_ && !drained();
-            stop_ = true;
+            cv_.wait(g, [&] { return ep_.drained() || ep_.lost(); });
+            lost_pending = ep_.lost() && !ep_.drained();
         }
-        cv_.notify_all();
-        if (thread_.joinable()) thread_.join();
+        pump_->stop();
         if (lost_pending) throw LSPError("connection lost before pending messages were acknowledged");
     }
 
    private:
-    using clock = std::chrono::steady_clock;
-
-    void send(const Message& m) { conn_->write(m.Marshal()); }
-    bool drained() const { return pending_.empty() && unacked_.empty(); }
-    bool window_open() const {
-        const int64_t base = unacked_.empty() ? next_seq_ : unacked_.begin()->first;
-        return next_seq_ < base + w_;
-    }
-    void pump() {  // caller holds mu_
-        while (!pending_.empty() && window_open()) {
-            Message m = NewData(id_, next_seq_, std::move(pending_.front()));
-            pending_.pop_front();
-            unacked_.emplace(next_seq_++, m);
-            send(m);
-        }
-    }
-    void on_message(const Message& m) {  // caller holds mu_
-        idle_ = 0;
-        if (m.Type == MsgType::Ack) {
-            if (unacked_.erase(m.SeqNum)) pump();
-            return;
-        }
-        if (m.Type != MsgType::Data || m.SeqNum < 1) return;
-        const int64_t s = m.SeqNum;
-        if (s >= expect_ + w_) return;  // beyond the receive window: discard
-        send(NewAck(id_, s));
-        if (std::find(recent_.begin(), recent_.end(), s) == recent_.end()) {
-            recent_.push_back(s);
-            if ((int)recent_.size() > w_) recent_.pop_front();
-        }
-        got_data_ = true;
-        if (s >= expect_) ooo_.emplace(s, m.Payload.value_or(""));
-        bool any = false;
-        for (auto it = ooo_.find(expect_); it != ooo_.end(); it = ooo_.find(expect_)) {
-            reads_.push_back(std::move(it->second));
-            ooo_.erase(it);
-            ++expect_;
-            any = true;
-        }
-        if (any) cv_.notify_all();
-    }
-    void on_epoch() {  // caller holds mu_
-        if (lost_) return;
-        if (++idle_ >= k_) {
-            lost_ = true;
-            cv_.notify_all();
-            return;
-        }
-        if (!got_data_) send(NewAck(id_, 0));
-        for (const auto& kv : unacked_) send(kv.second);
-        for (int64_t s : recent_) send(NewAck(id_, s));
-    }
-    void loop() {
-        const auto period = std::chrono::milliseconds(p_.EpochMillis);
-        auto next = clock::now() + period;
-        for (;;) {
-            {
-                std::lock_guard<std::mutex> g(mu_);
-                if (stop_) return;
-                if (clock::now() >= next) {
-                    next += period;
-                    on_epoch();
-                }
-            }
-            const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(next - clock::now()).count();
-            const auto got = conn_->read((int)std::clamp<long long>(left, 0, 50));
-            if (!got) continue;
-            Message m;
-            try {
-                m = Message::Unmarshal(*got);
-            } catch (const bmjson::DecodeError&) {
-                continue;
-            }
-            std::lock_guard<std::mutex> g(mu_);
-            if (m.ConnID != id_ || lost_) continue;
-            on_message(m);
-        }
-    }
-
-    std::unique_ptr<detail::Conn> conn_;
-    const Params p_;
-    const int64_t id_;
-    const int w_, k_;
+    std::unique_ptr<detail::Socket> sock_;
     std::mutex mu_;
     std::condition_variable cv_;
-    std::thread thread_;
-    int64_t next_seq_ = 1, expect_ = 1;
-    std::deque<std::string> pending_, reads_;
-    std::map<int64_t, Message> unacked_;
-    std::map<int64_t, std::string> ooo_;
-    std::deque<int64_t> recent_;
-    bool got_data_ = false, lost_ = false, closing_ = false, stop_ = false;
-    int idle_ = 0;
+    detail::Endpoint ep_;
+    std::deque<std::string> reads_;
+    bool closing_ = false;
+    std::unique_ptr<detail::Pump> pump_;  // last: its thread stops before the state above goes
 };
 
 // client_impl.go:52 / README:111-138: blocks until the server acknowledges
 // the connection; LSPError after EpochLimit epochs without an Ack.
 inline std::unique_ptr<Client> NewClient(const std::string& hostport, const Params& p = Params{}) {
-    auto conn = std::make_unique<detail::Conn>(hostport);
+    auto sock = detail::Socket::dial(hostport);
     const std::string connect = NewConnect().Marshal();
     for (int e = 0; e < std::max(1, p.EpochLimit); ++e) {
-        conn->write(connect);
+        sock->write(connect);
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(p.EpochMillis);
         for (;;) {
             const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(
                                   deadline - std::chrono::steady_clock::now())
                                   .count();
             if (left <= 0) break;
-            const auto got = conn->read((int)left);
+            const auto got = sock->read((int)left);
             if (!got) continue;
-            try {
-                const Message m = Message::Unmarshal(*got);
-                if (m.Type == MsgType::Ack && m.SeqNum == 0 && m.ConnID > 0)
-                    return std::make_unique<Client>(std::move(conn), m.ConnID, p);
-            } catch (const bmjson::DecodeError&) {
-            }
+            const auto m = detail::parse(got->first);
+            if (m && m->Type == MsgType::Ack && m->SeqNum == 0 && m->ConnID > 0)
+                return std::make_unique<Client>(std::move(sock), m->ConnID, p);
         }
     }
     throw LSPError("could not connect to " + hostport);
+}
+
+// A Server error: conn_id is the connection it concerns, 0 for the server
+// itself (server_api.go:13-17).
+class ServerError : public LSPError {
+   public:
+    ServerError(const std::string& what, int64_t conn_id) : LSPError(what), conn_id_(conn_id) {}
+    int64_t conn_id() const { return conn_id_; }
+
+   private:
+    int64_t conn_id_;
+};
+
+// server_api.go:6-39.  Create with NewServer.
+class Server {
+   public:
+    Server(std::unique_ptr<detail::Socket> sock, const Params& p) : sock_(std::move(sock)), p_(p) {
+        port_ = sock_->local_port();
+        pump_ = std::make_unique<detail::Pump>(
+            *sock_, p.EpochMillis, mu_, [this] { on_epoch(); },
+            [this](std::string raw, std::string from) { on_packet(raw, from); });
+    }
+    Server(const Server&) = delete;
+    Server& operator=(const Server&) = delete;
+    ~Server() { pump_->stop(); }
+
+    int port() const { return port_; }
+
+    // -> (conn_id, payload).  ServerError(conn_id) when a client connection
+    // is lost, ServerError(0) once the server is closed.
+    std::pair<int64_t, std::string> Read() {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return !reads_.empty() || closed_; });
+        if (reads_.empty()) throw ServerError("server closed", 0);
+        auto [cid, payload] = std::move(reads_.front());
+        reads_.pop_front();
+        if (!payload) throw ServerError("connection " + std::to_string(cid) + " lost", cid);
+        return {cid, std::move(*payload)};
+    }
+
+    // Non-blocking; ServerError if the connection does not exist or is lost.
+    void Write(int64_t conn_id, std::string payload) {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = conns_.find(conn_id);
+        if (it == conns_.end() || it->second->ep.lost() || it->second->user_closed)
+            throw ServerError("connection " + std::to_string(conn_id) + " does not exist", conn_id);
+        it->second->ep.write(std::move(payload));
+    }
+
+    // Non-blocking: pending messages still go out; nothing more is read.
+    void CloseConn(int64_t conn_id) {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = conns_.find(conn_id);
+        if (it == conns_.end() || it->second->user_closed)
+            throw ServerError("connection " + std::to_string(conn_id) + " does not exist", conn_id);
+        it->second->user_closed = it->second->closing = true;
+        reads_.erase(std::remove_if(reads_.begin(), reads_.end(), [&](const auto& r) { return r.first == conn_id; }),
+                     reads_.end());
+        drop_if_done(conn_id);
+    }
+
+    // Blocks until every client's pending messages are acknowledged or that
+    // client is lost; ServerError(0) if any was lost meanwhile.
+    void Close() {
+        bool lost_any;
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            closed_ = true;
+            for (auto& kv : conns_) kv.second->closing = true;
+            cv_.notify_all();
+            cv_.wait(g, [&] {
+                return std::all_of(conns_.begin(), conns_.end(),
+                                   [](const auto& kv) { return kv.second->ep.drained() || kv.second->ep.lost(); });
+            });
+            lost_any = lost_any_;
+        }
+        pump_->stop();
+        if (lost_any) throw ServerError("a client was lost with messages pending", 0);
+    }
+
+   private:
+    struct Conn {
+        Conn(int64_t id, const Params& p, detail::Socket& s, std::string a)
+            : addr(std::move(a)), ep(id, p, [&s, this](const Message& m) { s.write(m.Marshal(), addr); }) {}
+        std::string addr;
+        detail::Endpoint ep;
+        bool closing = false;      // CloseConn / Close: finish sending, then drop
+        bool user_closed = false;  // CloseConn: deliver nothing more from it
+    };
+
+    void forget(int64_t cid) {
+        auto it = conns_.find(cid);
+        if (it == conns_.end()) return;
+        by_addr_.erase(it->second->addr);
+        conns_.erase(it);
+    }
+    void drop_if_done(int64_t cid) {
+        auto it = conns_.find(cid);
+        if (it != conns_.end() && it->second->closing && it->second->ep.drained()) forget(cid);
+    }
+    void on_packet(const std::string& raw, const std::string& from) {
+        const auto m = detail::parse(raw);
+        if (!m) return;
+        if (m->Type == MsgType::Connect) {
+            auto a = by_addr_.find(from);
+            int64_t cid;
+            if (a == by_addr_.end()) {
+                if (closed_) return;
+                cid = next_id_++;
+                conns_.emplace(cid, std::make_unique<Conn>(cid, p_, *sock_, from));
+                by_addr_.emplace(from, cid);
+            } else {
+                cid = a->second;
+            }
+            sock_->write(NewAck(cid, 0).Marshal(), from);  // a repeated Connect gets the same id
+            return;
+        }
+        auto it = conns_.find(m->ConnID);
+        if (it == conns_.end() || it->second->addr != from || it->second->ep.lost()) return;
+        std::deque<std::string> out;
+        it->second->ep.on_message(*m, out);
+        if (!it->second->user_closed)
+            for (auto& p : out) reads_.emplace_back(m->ConnID, std::move(p));
+        drop_if_done(m->ConnID);
+        cv_.notify_all();
+    }
+    void on_epoch() {
+        std::vector<int64_t> ids;
+        for (const auto& kv : conns_) ids.push_back(kv.first);
+        for (int64_t cid : ids) {
+            Conn& c = *conns_.at(cid);
+            if (c.ep.on_epoch()) {
+                if (!c.ep.drained()) lost_any_ = true;
+                if (!c.user_closed) reads_.emplace_back(cid, std::nullopt);
+                forget(cid);
+            } else {
+                drop_if_done(cid);
+            }
+        }
+        cv_.notify_all();
+    }
+
+    std::unique_ptr<detail::Socket> sock_;
+    const Params p_;
+    int port_ = 0;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::map<int64_t, std::unique_ptr<Conn>> conns_;
+    std::map<std::string, int64_t> by_addr_;
+    int64_t next_id_ = 1;
+    std::deque<std::pair<int64_t, std::optional<std::string>>> reads_;  // nullopt payload: that conn was lost
+    bool closed_ = false, lost_any_ = false;
+    std::unique_ptr<detail::Pump> pump_;  // last: its thread stops before the state above goes
+};
+
+// server_impl.go:48: starts listening (port 0 = any free port, see
+// Server::port) and returns without blocking.
+inline std::unique_ptr<Server> NewServer(int port, const Params& p = Params{}, const std::string& host = "127.0.0.1") {
+    return std::make_unique<Server>(detail::Socket::listen(port, host), p);
 }
 
 }  // namespace lsp

@@ -19,6 +19,7 @@ from distributed_bitcoin_minter_amd.bitcoin import Message, MsgType, NewJoin, Ne
 
 EXE = os.path.join(ROOT, "examples", "bm_miner")
 CLIENT = os.path.join(ROOT, "examples", "bm_client")
+SERVER = os.path.join(ROOT, "examples", "bm_server")
 _HDRS = [os.path.join(ROOT, "include", h) for h in ("btcminer.hpp", "btcminer.h", "bm_json.hpp", "lsp.hpp")]
 
 
@@ -40,6 +41,10 @@ def _exe():
 
 def _client():
     return _build(CLIENT, os.path.join(ROOT, "examples", "bm_client.cpp"), False)
+
+
+def _server():
+    return _build(SERVER, os.path.join(ROOT, "examples", "bm_server.cpp"), False)
 
 
 def _selftest(lines):
