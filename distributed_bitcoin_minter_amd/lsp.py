@@ -138,6 +138,33 @@ class LSPError(Exception):
         self.conn_id = conn_id
 
 
+def _next_tick(due, period):
+    """The deadline after the tick that was due at `due`.  Like Go's
+    time.Ticker, ticks missed while the process was descheduled are dropped,
+    not fired back to back: a burst of K catch-up epochs would declare a
+    connection lost that was silent for one stall, not for K epochs."""
+    nxt = due + period
+    now = time.monotonic()
+    return nxt if nxt > now else now + period
+
+
+def _drain(conn, handle, limit=4096):
+    """Before an epoch counts silence, handle the datagrams already queued in
+    the socket (lock held).  The reader thread may not have been scheduled
+    for a while (GIL, a busy host); what waits unread was heard, and an epoch
+    that ignored it could declare a live peer lost.  UDP hands each datagram
+    to one reader, so the reader thread and this drain never both see one;
+    the reordering between them is what LSP's sequence numbers absorb."""
+    for _ in range(limit):
+        try:
+            got = conn.read_from(block=False)
+        except OSError:
+            return
+        if got is None:
+            return
+        handle(*got)
+
+
 class _Endpoint:
     """Protocol state of one end of one connection (no I/O of its own)."""
 
@@ -244,15 +271,18 @@ class Client:
                 continue
             except OSError:
                 break
-            try:
-                m = Message.unmarshal(data)
-            except (ValueError, KeyError):
-                continue
             with self._lock:
-                if m.ConnID != self._ep.id or self._ep.lost:
-                    continue
-                self._reads.extend(self._ep.on_message(m))
-                self._lock.notify_all()
+                self._handle(data)
+
+    def _handle(self, data):  # lock held
+        try:
+            m = Message.unmarshal(data)
+        except (ValueError, KeyError):
+            return
+        if m.ConnID != self._ep.id or self._ep.lost:
+            return
+        self._reads.extend(self._ep.on_message(m))
+        self._lock.notify_all()
 
     def _epochs(self):
         period = self._params.EpochMillis / 1000.0
@@ -263,7 +293,8 @@ class Client:
                 if left > 0:
                     self._lock.wait(timeout=left)  # woken early by other events: re-check the deadline
                     continue
-                nxt += period
+                nxt = _next_tick(nxt, period)
+                _drain(self._conn, lambda data, addr: self._handle(data))
                 self._ep.on_epoch()
                 self._lock.notify_all()
 
@@ -389,30 +420,33 @@ class Server:
                 continue
             except OSError:
                 break
-            try:
-                m = Message.unmarshal(data)
-            except (ValueError, KeyError):
-                continue
             with self._lock:
-                if m.Type == MsgConnect:
-                    cid = self._by_addr.get(addr)
-                    if cid is None:
-                        if self._closed:
-                            continue
-                        cid = self._next_id
-                        self._next_id += 1
-                        self._conns[cid] = _ServerConn(_Endpoint(cid, self._params, self._sender(addr)), addr)
-                        self._by_addr[addr] = cid
-                    self._conns[cid].ep.send(NewAck(cid, 0))  # a duplicate Connect gets the same id
-                    continue
-                c = self._conns.get(m.ConnID)
-                if c is None or c.addr != addr or c.ep.lost:
-                    continue
-                out = c.ep.on_message(m)
-                if not c.user_closed:
-                    self._reads.extend((m.ConnID, p) for p in out)
-                self._drop_if_done(m.ConnID)
-                self._lock.notify_all()
+                self._handle(data, addr)
+
+    def _handle(self, data, addr):  # lock held
+        try:
+            m = Message.unmarshal(data)
+        except (ValueError, KeyError):
+            return
+        if m.Type == MsgConnect:
+            cid = self._by_addr.get(addr)
+            if cid is None:
+                if self._closed:
+                    return
+                cid = self._next_id
+                self._next_id += 1
+                self._conns[cid] = _ServerConn(_Endpoint(cid, self._params, self._sender(addr)), addr)
+                self._by_addr[addr] = cid
+            self._conns[cid].ep.send(NewAck(cid, 0))  # a duplicate Connect gets the same id
+            return
+        c = self._conns.get(m.ConnID)
+        if c is None or c.addr != addr or c.ep.lost:
+            return
+        out = c.ep.on_message(m)
+        if not c.user_closed:
+            self._reads.extend((m.ConnID, p) for p in out)
+        self._drop_if_done(m.ConnID)
+        self._lock.notify_all()
 
     def _epochs(self):
         period = self._params.EpochMillis / 1000.0
@@ -423,7 +457,8 @@ class Server:
                 if left > 0:
                     self._lock.wait(timeout=left)
                     continue
-                nxt += period
+                nxt = _next_tick(nxt, period)
+                _drain(self._conn, self._handle)
                 for cid, c in list(self._conns.items()):
                     if c.ep.on_epoch():
                         if not c.ep.drained():

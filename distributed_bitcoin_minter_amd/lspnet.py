@@ -9,6 +9,7 @@ Here a connection's role is fixed when it is created (``listen`` -> server,
 ``dial`` -> client).  Dropping is decided per packet with a module-level RNG
 that tests may seed (``seed``), so a fault-injection run can be replayed.
 """
+import os
 import random
 import socket
 import threading
@@ -79,7 +80,15 @@ class UDPConn:
     """A UDP socket with lspnet's drop semantics for its role."""
 
     def __init__(self, sock, is_server, peer=None):
+        # Always in timeout mode (CPython then keeps the fd O_NONBLOCK and
+        # emulates blocking with poll), so a second handle on the same socket
+        # can read without blocking: read_from(block=False) uses it, and
+        # CPython's timeout path would first poll for up to the timeout.
+        if sock.gettimeout() is None:
+            sock.settimeout(3600.0)
         self._sock = sock
+        self._nb = socket.socket(sock.family, sock.type, sock.proto, fileno=os.dup(sock.fileno()))
+        self._nb.setblocking(False)
         self._server = is_server
         self._peer = peer
         self._closed = False
@@ -92,13 +101,21 @@ class UDPConn:
         return self._sock.getsockname()[1]
 
     def settimeout(self, t):
-        self._sock.settimeout(t)
+        self._sock.settimeout(t if t is not None else 3600.0)
 
-    def read_from(self):
-        """Next packet not dropped: (bytes, addr).  Raises socket.timeout / OSError."""
+    def read_from(self, block=True):
+        """Next packet not dropped: (bytes, addr).  Raises socket.timeout /
+        OSError; with block=False, None when nothing is queued."""
         key = "server_read" if self._server else "client_read"
         while True:
-            data, addr = self._sock.recvfrom(MAX_PACKET)
+            try:
+                data, addr = (self._sock if block else self._nb).recvfrom(MAX_PACKET)
+            except (BlockingIOError, InterruptedError):
+                return None
+            except ConnectionRefusedError:
+                # a connected client socket reports an earlier send's ICMP
+                # port-unreachable here: for UDP that is only a lost packet
+                continue
             if _drop_it(key):
                 if _debug:
                     print(f"DROPPING read packet of length {len(data)}", flush=True)
@@ -114,7 +131,7 @@ class UDPConn:
             return len(data)
         try:
             if addr is None:
-                self._sock.sendto(data, self._peer)
+                self._sock.send(data)
             else:
                 self._sock.sendto(data, addr)
         except OSError:
@@ -124,12 +141,30 @@ class UDPConn:
     def close(self):
         if not self._closed:
             self._closed = True
+            self._nb.close()
             self._sock.close()
+
+
+# Receive buffers.  One server socket takes every client's datagrams, and a
+# Python reader that is descheduled for a few tens of ms (GC, a busy host) lets
+# the kernel's default ~200 KB fill up: the overflow drops look like network
+# loss and the retransmissions they trigger add load.  The kernel caps these
+# at net.core.rmem_max.
+SERVER_RCVBUF = 4 << 20
+CLIENT_RCVBUF = 1 << 20
+
+
+def _rcvbuf(s, n):
+    try:
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, n)
+    except OSError:
+        pass  # the default buffer still works
 
 
 def listen(port, host="127.0.0.1"):
     """ListenUDP for a server (net.go:37-52).  port 0 picks a free port."""
     s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    _rcvbuf(s, SERVER_RCVBUF)
     s.bind((host, port))
     return UDPConn(s, True)
 
@@ -141,5 +176,9 @@ def dial(hostport):
         host = "127.0.0.1"
     peer = (socket.gethostbyname(host), int(port))
     s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    _rcvbuf(s, CLIENT_RCVBUF)
     s.bind(("0.0.0.0" if peer[0] != "127.0.0.1" else "127.0.0.1", 0))
+    # connected, as Go's DialUDP: the kernel then delivers only the server's
+    # datagrams, never a stale peer's that still targets a reused local port
+    s.connect(peer)
     return UDPConn(s, False, peer)

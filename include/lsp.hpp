@@ -313,7 +313,14 @@ class Socket {
     }
 
    private:
-    Socket(int fd, bool server) : fd_(fd), server_(server) {}
+    // A server socket takes every client's datagrams: a larger receive buffer
+    // keeps a reader descheduled for a few tens of ms from overflowing the
+    // kernel's default (~200 KB) into drops that look like network loss.
+    // The kernel caps the request at net.core.rmem_max.
+    Socket(int fd, bool server) : fd_(fd), server_(server) {
+        const int bytes = server ? (4 << 20) : (1 << 20);
+        (void)::setsockopt(fd_, SOL_SOCKET, SO_RCVBUF, &bytes, sizeof bytes);
+    }
     int fd_;
     bool server_;
 };
@@ -413,7 +420,10 @@ class Pump {
         auto next = clock::now() + period_;
         while (!stop_) {
             if (clock::now() >= next) {
+                // like Go's time.Ticker: ticks missed during a stall are dropped,
+                // not fired back to back (K of them would fake K silent epochs)
                 next += period_;
+                if (next <= clock::now()) next = clock::now() + period_;
                 std::lock_guard<std::mutex> g(mu_);
                 on_epoch_();
             }
