@@ -152,6 +152,46 @@ def fold_sgpr_constants(lines, kernels):
     return out, n_fold, n_split
 
 
+def drop_dead_smov(lines, kernels):
+    """Delete s_mov_b32 sN, imm that the literal fold left dead: inside one
+    block, sN is written again by another s_mov_b32 before anything else
+    names sN.  Any other appearance of sN (as a source, a destination of
+    another op, inside a register range or in inline asm) counts as a use, so
+    the rule only ever removes a write nothing can read."""
+    out, n = list(lines), 0
+    in_kernel = False
+    pending = {}  # sN -> index in out of its last s_mov_b32 with no use since
+    dead = set()
+    mov_re = re.compile(r"^\s+s_mov_b32 s(\d+), (\S+)\s*$")
+    for i, ln in enumerate(lines):
+        m_fn = re.match(r"^(_Z\S+):", ln)
+        if m_fn:
+            in_kernel = any(k in m_fn.group(1) for k in kernels)
+            pending = {}
+            continue
+        if ln.startswith(".Lfunc_end"):
+            in_kernel = False
+        if not in_kernel:
+            continue
+        if re.match(r"^[.%$\w]+:", ln) or ln.startswith("; %bb") or re.match(r"^\s+s_(cbranch|branch|setpc|swappc)", ln):
+            pending = {}
+            continue
+        code = ln.split(";")[0]
+        m = mov_re.match(code)
+        if m and IMM_RE.match(m.group(2)):
+            r = int(m.group(1))
+            if r in pending:
+                dead.add(pending[r])
+            pending[r] = i
+            continue
+        for r in [int(x[1:]) for x in _regs(code) if x.startswith("s")]:
+            pending.pop(r, None)
+    for i in sorted(dead, reverse=True):
+        del out[i]
+        n += 1
+    return out, n
+
+
 def split_add3(lines, kernels, every):
     """Split every `every`-th all-VGPR v_add3_u32 d, a, b, c of the search
     kernels into v_add_u32 d, x, y; v_add_u32 d, z, d.  The loop is slow-slot
@@ -359,6 +399,8 @@ def main():
     ap.add_argument("--kernels", default="search_kernel")
     ap.add_argument("--min-fast-run", type=int, default=1)
     ap.add_argument("--fold-sgpr", type=int, default=1, help="1: literal-fold known SGPR constants, split add3")
+    ap.add_argument("--drop-dead-smov", type=int, default=0,
+                    help="1: delete the s_mov_b32 sN, imm the fold left with no reader before the next one")
     ap.add_argument("--split-add3-every", type=int, default=0,
                     help="K > 0: split every K-th all-VGPR v_add3_u32 into two v_add_u32")
     ap.add_argument("--cluster", type=int, default=-1,
@@ -369,6 +411,9 @@ def main():
     if a.fold_sgpr:
         lines, n_fold, n_split = fold_sgpr_constants(lines, a.kernels.split(","))
         print(f"bm_prio: {a.src}: {n_fold} SGPR constants folded, {n_split} v_add3 split", file=sys.stderr)
+    if a.drop_dead_smov:
+        lines, n_dead = drop_dead_smov(lines, a.kernels.split(","))
+        print(f"bm_prio: {a.src}: {n_dead} dead s_mov_b32 removed", file=sys.stderr)
     if a.split_add3_every:
         lines, n_split3 = split_add3(lines, a.kernels.split(","), a.split_add3_every)
         print(f"bm_prio: {a.src}: {n_split3} all-VGPR v_add3 split", file=sys.stderr)

@@ -308,3 +308,31 @@ def test_cluster_schedule_respects_war_and_scc():
         regs = {f"v{i}": rng.getrandbits(32) for i in range(10)}
         regs.update({f"s{i}": rng.getrandbits(32) for i in range(10)})
         assert _interp(blk, regs) == _interp(out, regs)
+
+
+def test_drop_dead_smov_keeps_the_inner_loop():
+    """--drop-dead-smov removes only s_mov_b32 writes that a later s_mov_b32
+    of the same SGPR in the block overwrites with no read between: the real C2
+    inner loop leaves every register (the removed SGPRs included, whose last
+    write stays) as before, on random inputs; a read between two writes, and
+    a block boundary, keep the first write."""
+    import glob
+    srcs = glob.glob(os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc", "build", "inst1_16_23.dev.s"))
+    if not srcs:
+        pytest.skip("device assembly not built (make -C distributed_bitcoin_minter_amd/csrc)")
+    lines, _, _ = bm_prio.fold_sgpr_constants(open(srcs[0]).readlines(), ["search_kernel"])
+    kern = "_ZN2bm13search_kernelILi18ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:"
+    dropped, n = bm_prio.drop_dead_smov(lines, ["search_kernel"])
+    before, after = _inner_block_from(lines, kern), _inner_block_from(dropped, kern)
+    assert n > 0 and len(after) < len(before)
+    assert all(ln.strip().startswith("s_mov_b32") for ln in set(before) - set(after))
+    rng = random.Random(9)
+    for _ in range(10):
+        regs = {f"v{i}": rng.getrandbits(32) for i in range(256)}
+        regs.update({f"s{i}": rng.getrandbits(32) for i in range(106)})
+        assert _interp(before, regs) == _interp(after, regs)
+    blk = ["_Z3foo:\n", "\ts_mov_b32 s4, 1\n", "\tv_add_u32_e32 v1, s4, v1\n", "\ts_mov_b32 s4, 2\n",
+           "\ts_mov_b32 s5, 3\n", ".LBB0_1:\n", "\ts_mov_b32 s5, 4\n", "\ts_mov_b32 s6, 5\n",
+           "\ts_mov_b32 s6, 6\n", ".Lfunc_end0:\n"]
+    out, n = bm_prio.drop_dead_smov(blk, ["foo"])
+    assert n == 1 and "\ts_mov_b32 s6, 5\n" not in out and len(out) == len(blk) - 1
