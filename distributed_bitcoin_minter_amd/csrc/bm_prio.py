@@ -152,7 +152,7 @@ def fold_sgpr_constants(lines, kernels):
     return out, n_fold, n_split
 
 
-def drop_dead_smov(lines, kernels):
+def drop_dead_smov(lines, kernels, replace=None):
     """Delete s_mov_b32 sN, imm that the literal fold left dead: inside one
     block, sN is written again by another s_mov_b32 before anything else
     names sN.  Any other appearance of sN (as a source, a destination of
@@ -187,8 +187,40 @@ def drop_dead_smov(lines, kernels):
         for r in [int(x[1:]) for x in _regs(code) if x.startswith("s")]:
             pending.pop(r, None)
     for i in sorted(dead, reverse=True):
-        del out[i]
+        if replace is None:
+            del out[i]
+        else:
+            out[i] = replace
         n += 1
+    return out, n
+
+
+def space_dependent_valu(lines, kernels):
+    """Insert s_nop 0 between two adjacent VALU ops of the search kernels'
+    big blocks when the second reads what the first wrote (an A/B probe of
+    whether the dead SALU writes the fold leaves behind help by spacing a
+    wave's dependent VALU)."""
+    out, in_kernel, prev, n = [], False, None, 0
+    for ln in lines:
+        m_fn = re.match(r"^(_Z\S+):", ln)
+        if m_fn:
+            in_kernel = any(k in m_fn.group(1) for k in kernels)
+            prev = None
+        elif ln.startswith(".Lfunc_end"):
+            in_kernel = False
+        du = _defs_uses(ln) if in_kernel else None
+        if du is None:
+            if in_kernel and ln.strip() and not ln.strip().startswith(";"):
+                prev = None
+            out.append(ln)
+            continue
+        mn, defs, uses = du
+        if mn.startswith("v_"):
+            if prev is not None and prev & uses:
+                out.append("\ts_nop 0\n")
+                n += 1
+            prev = defs
+        out.append(ln)
     return out, n
 
 
@@ -400,7 +432,10 @@ def main():
     ap.add_argument("--min-fast-run", type=int, default=1)
     ap.add_argument("--fold-sgpr", type=int, default=1, help="1: literal-fold known SGPR constants, split add3")
     ap.add_argument("--drop-dead-smov", type=int, default=0,
-                    help="1: delete the s_mov_b32 sN, imm the fold left with no reader before the next one")
+                    help="1: delete the s_mov_b32 sN, imm the fold left with no reader before the next one; "
+                         "2: replace each by s_nop 0 (measured: 1 is C2 -0.7%%, profiles/r02/ab_dead_smov.log)")
+    ap.add_argument("--space-dependent", type=int, default=0,
+                    help="1: s_nop 0 between adjacent VALU where the second reads the first's result")
     ap.add_argument("--split-add3-every", type=int, default=0,
                     help="K > 0: split every K-th all-VGPR v_add3_u32 into two v_add_u32")
     ap.add_argument("--cluster", type=int, default=-1,
@@ -412,8 +447,12 @@ def main():
         lines, n_fold, n_split = fold_sgpr_constants(lines, a.kernels.split(","))
         print(f"bm_prio: {a.src}: {n_fold} SGPR constants folded, {n_split} v_add3 split", file=sys.stderr)
     if a.drop_dead_smov:
-        lines, n_dead = drop_dead_smov(lines, a.kernels.split(","))
-        print(f"bm_prio: {a.src}: {n_dead} dead s_mov_b32 removed", file=sys.stderr)
+        lines, n_dead = drop_dead_smov(lines, a.kernels.split(","), "\ts_nop 0\n" if a.drop_dead_smov == 2 else None)
+        print(f"bm_prio: {a.src}: {n_dead} dead s_mov_b32 {'removed' if a.drop_dead_smov == 1 else 'made s_nop 0'}",
+              file=sys.stderr)
+    if a.space_dependent:
+        lines, n_sp = space_dependent_valu(lines, a.kernels.split(","))
+        print(f"bm_prio: {a.src}: {n_sp} s_nop 0 between dependent VALU", file=sys.stderr)
     if a.split_add3_every:
         lines, n_split3 = split_add3(lines, a.kernels.split(","), a.split_add3_every)
         print(f"bm_prio: {a.src}: {n_split3} all-VGPR v_add3 split", file=sys.stderr)
