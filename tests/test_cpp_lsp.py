@@ -16,8 +16,10 @@ GPU: the C++ miner process (bm_miner host:port) joins the Python server and
 answers clients' requests bit-exact with the oracle under 10% drops, then
 shuts down once the server is gone (README:412)."""
 import json
+import os
 import socket
 import subprocess
+import sys
 import threading
 import time
 
@@ -26,7 +28,8 @@ import pytest
 from distributed_bitcoin_minter_amd import lsp, lspnet, miner
 from distributed_bitcoin_minter_amd.bitcoin import Message, MsgType, NewJoin, NewRequest, NewResult, _as_bytes
 from distributed_bitcoin_minter_amd.server import BitcoinServer
-from test_cpp_host import _client, _exe
+from conftest import ROOT
+from test_cpp_host import _build, _client, _exe
 
 KNOWN = [("bradfitz", 9999, "Result 1419516646206828 9898"), ("msg", 2, "Result 4754799531757243342 1")]
 
@@ -222,3 +225,21 @@ def test_cpp_gpu_miner_in_the_system(oracle):
             raise
         assert m.returncode == 0, err
         assert b"lost contact with the server" in err
+
+
+@pytest.mark.gpu
+def test_c5_native_at_size():
+    """BASELINE C5 at full size with every process native: the C++ server,
+    4 C++ GPU miners on device 0, 16 C++ clients asking for [0, 2^34-1] of
+    "client-%02d", 2^32-nonce jobs, 10% read and write drop at every endpoint
+    (tools/bench_c5_native.py).  Every answer equals the full CPU scan of
+    that client's range (tests/golden/c5_clients.json)."""
+    import json
+    _exe(), _client(), _build(os.path.join(ROOT, "examples", "bm_server"),
+                              os.path.join(ROOT, "examples", "bm_server.cpp"), False)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_c5_native.py"), "--timeout", "200"],
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["all_answered"] and out["golden_ok"] and out["golden_checked"] == 16, out
+    print(f"C5 native: {out['GHs']} GH/s end to end over {out['seconds']} s")
