@@ -499,3 +499,32 @@ def test_client_close(nclients):
     assert (cid, d) == (c.ConnID(), b"again")
     c.Close()
     srv.Close()
+
+
+@pytest.mark.parametrize("side", ["server", "client"])
+def test_stalled_reader_thread_does_not_lose_a_live_peer(monkeypatch, side):
+    """An endpoint's reader thread descheduled for 50 epochs (here: asleep)
+    must not make it count the peer silent: each epoch first handles the
+    datagrams queued in its socket (lsp._drain), so the connection forms,
+    data flows both ways, and nobody is declared lost (K = 5 epochs)."""
+    cls = lsp.Server if side == "server" else lsp.Client
+    orig = cls._reader
+
+    def stalled(self):
+        time.sleep(1.0)
+        orig(self)
+    monkeypatch.setattr(cls, "_reader", stalled)
+    p = params(w=2, ms=20, k=5)
+    srv = lsp.NewServer(0, p)
+    c = lsp.NewClient(f"127.0.0.1:{srv.port}", p)
+    for i in range(5):
+        c.Write(b"ping-%d" % i)
+    got = [srv.Read() for _ in range(5)]
+    assert [d for _, d in got] == [b"ping-%d" % i for i in range(5)]
+    srv.Write(got[0][0], b"pong")
+    assert c.Read() == b"pong"
+    time.sleep(0.3)  # 15 epochs with the reader still asleep: still connected
+    c.Write(b"again")
+    assert srv.Read()[1] == b"again"
+    c.Close()
+    srv.Close()
