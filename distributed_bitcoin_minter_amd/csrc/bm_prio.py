@@ -422,6 +422,20 @@ def run(lines, kernels, slow, fast, min_fast_run=1):
     return out, n_toggle, n_valu
 
 
+def lead_toggles(lines, prio):
+    """Move every `s_setprio <prio>` one VALU earlier: above the last op of
+    the run it ends, when that run has at least two VALU (an A/B probe of the
+    toggle's timing relative to the ops it reorders)."""
+    out = list(lines)
+    n = 0
+    is_valu = lambda ln: ln.lstrip().startswith("v_")
+    for i in range(2, len(out)):
+        if out[i].strip() == f"s_setprio {prio}" and is_valu(out[i - 1]) and is_valu(out[i - 2]):
+            out[i - 1], out[i] = out[i], out[i - 1]
+            n += 1
+    return out, n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
@@ -434,6 +448,8 @@ def main():
     ap.add_argument("--drop-dead-smov", type=int, default=0,
                     help="1: delete the s_mov_b32 sN, imm the fold left with no reader before the next one; "
                          "2: replace each by s_nop 0 (measured: 1 is C2 -0.7%%, profiles/r02/ab_dead_smov.log)")
+    ap.add_argument("--lead-slow", type=int, default=0, help="1: each s_setprio <slow> one VALU earlier")
+    ap.add_argument("--lead-fast", type=int, default=0, help="1: each s_setprio <fast> one VALU earlier")
     ap.add_argument("--space-dependent", type=int, default=0,
                     help="1: s_nop 0 between adjacent VALU where the second reads the first's result")
     ap.add_argument("--split-add3-every", type=int, default=0,
@@ -459,6 +475,10 @@ def main():
     if a.cluster >= 0:
         lines = cluster_runs(lines, a.kernels.split(","), max_run=a.cluster)
     out, n_toggle, n_valu = run(lines, a.kernels.split(","), a.slow_prio, a.fast_prio, a.min_fast_run)
+    for prio, on in ((a.slow_prio, a.lead_slow), (a.fast_prio, a.lead_fast)):
+        if on:
+            out, n_lead = lead_toggles(out, prio)
+            print(f"bm_prio: {a.src}: {n_lead} s_setprio {prio} moved one VALU earlier", file=sys.stderr)
     open(a.dst, "w").writelines(out)
     print(f"bm_prio: {a.src}: {n_toggle} s_setprio over {n_valu} VALU", file=sys.stderr)
 
