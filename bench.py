@@ -5,8 +5,11 @@ int32 VALU roofline).
 
 Workloads (--config):
   C2 (default, BASELINE configs[1])  msg "bradfitz", 2^32 nonces per GPU:
-      [0, N*2^32-1] over N GPUs, rank/device r scanning [r*2^32, (r+1)*2^32-1]
-      (weak scaling; at N = 1 exactly C2's [0, 2^32-1]).
+      [0, N*2^32-1] over N GPUs (weak scaling; at N = 1 exactly C2's
+      [0, 2^32-1]).  The pieces are contiguous; after the warmup they follow
+      each GPU's measured rate (the library's range partitioner, DESIGN.md
+      §6), so GPUs that clock differently finish together; --no-balance
+      keeps rank/device r on [r*2^32, (r+1)*2^32-1].
   C3 (configs[2])  the 120-byte message, 20-digit nonces:
       [2^64 - N*2^32, 2^64-1] (weak scaling).
   C4 (configs[3])  msg "bradfitz", [0, 2^40-1] split over the N GPUs
@@ -61,7 +64,7 @@ sys.path.insert(0, ROOT)
 
 from distributed_bitcoin_minter_amd import _lib  # noqa: E402
 from distributed_bitcoin_minter_amd._lib import Context, device_count, rccl_unique_id  # noqa: E402
-from distributed_bitcoin_minter_amd.dist import lex_min, rank_piece  # noqa: E402
+from distributed_bitcoin_minter_amd.dist import lex_min, rank_piece, shares_from_rates  # noqa: E402
 
 U64 = (1 << 64) - 1
 PER_GPU = 1 << 32
@@ -80,8 +83,8 @@ def workload(config, n):
     """(msg, lower, upper, scaling, description) of a config at n GPUs."""
     if config == "C2":
         return (MSG_C2, 0, n * PER_GPU - 1, "weak",
-                "C2: msg 'bradfitz', nonces [0, N*2^32-1], 2^32 per GPU (GPU r: [r*2^32, (r+1)*2^32-1]), "
-                "inclusive min (hash, nonce)")
+                "C2: msg 'bradfitz', nonces [0, N*2^32-1], 2^32 per GPU (N > 1: contiguous pieces in proportion to "
+                "each GPU's rate measured in the warmup, config.split), inclusive min (hash, nonce)")
     if config == "C3":
         return (M120, U64 - n * PER_GPU + 1, U64, "weak",
                 "C3: 120-byte msg, 20-digit nonces [2^64 - N*2^32, 2^64-1], 2^32 per GPU, inclusive min (hash, nonce)")
@@ -271,6 +274,40 @@ class Group:
             self.rdzv.close()
 
 
+# The range partitioner's shares for the torchrun ranks (None: near-equal
+# pieces).  Ranks of the library's RCCL group ("library": True) get them
+# through ctx.set_split; the rendezvous-gather paths cut their pieces with
+# dist.rank_piece, the mirror of the library's partitioner.
+SPLIT = {"shares": None, "library": False}
+
+
+def calibrate_split(args, ctx, grp):
+    """After the warmup: each GPU's rate in the last warmup step (its own
+    nonces over its launches' span, HIP events, so the wait for the other
+    ranks does not count) -> integer shares, the same on every rank -> the
+    timed steps cut the range in proportion (bm_ctx_set_split).
+    A one-process multi-device context balances itself (bm_ctx_set_balance).
+    Returns what the bench line reports."""
+    if args.no_balance or args.warmup < 1:
+        return {"mode": "near-equal"}
+    if grp.world == 1:
+        if ctx.num_devices() == 1:
+            return {"mode": "one device"}
+        sh = ctx.get_split()
+        return {"mode": "measured device rates (bm_ctx_set_balance)", "shares": sh} if sh else {"mode": "near-equal"}
+    st = ctx.last_stats()
+    rate = st.nonces / st.span_ms if st.span_ms > 0 and st.nonces >= (1 << 30) else 0.0
+    rates = grp.gather(rate)
+    if min(rates) <= 0:
+        return {"mode": "near-equal", "note": "a rank's piece was too small to time"}
+    shares = shares_from_rates(rates)
+    if SPLIT["library"]:
+        ctx.set_split(shares)
+    SPLIT["shares"] = shares
+    return {"mode": "measured rank rates, last warmup step", "shares": shares,
+            "rates_nonces_per_ms": [round(r, 1) for r in rates]}
+
+
 def open_contexts(args, world, rank, local):
     """(ctx, group, search, parallelism) for the launch mode (module docstring)."""
     if world > 1:
@@ -287,7 +324,7 @@ def open_contexts(args, world, rank, local):
             ctx = Context(devices=[dev])
 
             def search(msg, lo, hi):
-                piece = rank_piece(lo, hi, grp.rank, grp.world)
+                piece = rank_piece(lo, hi, grp.rank, grp.world, SPLIT["shares"])
                 part = ctx.search(msg, *piece) if piece else (U64, U64)
                 return lex_min(tuple(p) for p in grp.gather(list(part)))
             how = f"{world} processes (one per GPU), rendezvous gather of 16 B partials"
@@ -302,6 +339,7 @@ def open_contexts(args, world, rank, local):
             err = str(e)
         errs = [x for x in grp.gather(err) if x]
         if not errs:
+            SPLIT["library"] = True
             return ctx, grp, ctx.search, f"{world} processes (one per GPU), RCCL allgather of 16 B partials in-library"
         # every rank saw the failure: fall back to gathering the partials over
         # the rendezvous (the measurement is the same search; the combine is 16 B)
@@ -311,7 +349,7 @@ def open_contexts(args, world, rank, local):
         ctx = Context(devices=[local])
 
         def search(msg, lo, hi):
-            piece = rank_piece(lo, hi, grp.rank, grp.world)
+            piece = rank_piece(lo, hi, grp.rank, grp.world, SPLIT["shares"])
             part = ctx.search(msg, *piece) if piece else (U64, U64)
             return lex_min(tuple(p) for p in grp.gather(list(part)))
         return ctx, grp, search, (f"{world} processes (one per GPU), rendezvous gather of 16 B partials "
@@ -342,6 +380,8 @@ def main():
     ap.add_argument("--combine", default="rccl", choices=["rccl", "gather"],
                     help="torchrun ranks: in-library RCCL allgather (default) or a gather over the rendezvous")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-balance", action="store_true",
+                    help="keep near-equal pieces (default: after the warmup, pieces follow each GPU's measured rate)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N-way split on ONE GPU (all ranks / devices are GPU 0): exercises the multi-GPU "
                          "path on a one-GPU box; not a scaling measurement")
@@ -357,6 +397,8 @@ def main():
 
     ctx, grp, search, how = open_contexts(args, world, rank, local)
     ctx.set_timing(True)
+    if world == 1 and ctx.num_devices() > 1 and not args.no_balance:
+        ctx.set_balance(True)
     n = args.gpus
     msg, lo, hi, scaling, desc = workload(args.config, n)
 
@@ -372,6 +414,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    split = calibrate_split(args, ctx, grp)
     grp.barrier()
     t0 = time.perf_counter()
     doms = []
@@ -402,7 +445,7 @@ def main():
         "dtype": "u32",
         "data": "synthetic",
         "config": {"workload": desc, "name": args.config, "msg": msg.decode(), "lower": lo, "upper": hi,
-                   "global_nonces": total, "parallelism": how},
+                   "global_nonces": total, "parallelism": how, "split": split},
         "result": list(res),
         "golden": want,
         "result_ok": None if want is None else list(res) == want,

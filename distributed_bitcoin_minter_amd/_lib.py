@@ -20,7 +20,7 @@ BM_ENOMEM = -5
 BM_EINTERNAL = -6
 BM_MAX_LAUNCH_STATS = 64
 BM_RCCL_ID_BYTES = 128
-BM_ABI_VERSION = 3
+BM_ABI_VERSION = 4
 BM_COMBINE_AUTO, BM_COMBINE_RCCL, BM_COMBINE_HOST = 0, 1, 2
 U64_MAX = (1 << 64) - 1
 
@@ -97,6 +97,10 @@ def load():
         "bm_ctx_set_max_windows": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_ctx_set_combine": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_ctx_set_task_digits": ([vp, ctypes.c_int], ctypes.c_int),
+        "bm_ctx_set_split": ([vp, P(ctypes.c_uint32), ctypes.c_int], ctypes.c_int),
+        "bm_ctx_get_split": ([vp, P(ctypes.c_uint32), ctypes.c_int, P(ctypes.c_int)], ctypes.c_int),
+        "bm_ctx_set_balance": ([vp, ctypes.c_int], ctypes.c_int),
+        "bm_split_range": ([c_u64, c_u64, P(ctypes.c_uint32), ctypes.c_int, P(c_u64), P(c_u64)], ctypes.c_int),
         "bm_plan_segments": ([ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, P(Segment), ctypes.c_int,
                               P(ctypes.c_int)], ctypes.c_int),
         "bm_plan_segments_ex": ([ctypes.c_char_p, ctypes.c_size_t, c_u64, c_u64, ctypes.c_int, P(Segment),
@@ -144,6 +148,15 @@ def plan_segments(msg: bytes, lower: int, upper: int, max_windows: int = DEFAULT
     arr = (Segment * max(n.value, 1))()
     check(f(msg, len(msg), lower, upper, max_windows, arr, n.value, ctypes.byref(n)), "bm_plan_segments")
     return list(arr[: n.value])
+
+
+def split_range(lower: int, upper: int, n: int, shares=None):
+    """The library's partitioner (bm_split_range, pure CPU): n inclusive
+    pieces of [lower, upper], None for an empty one; shares None: near-equal."""
+    lo, hi = (c_u64 * n)(), (c_u64 * n)()
+    sh = (ctypes.c_uint32 * n)(*shares) if shares is not None else None
+    check(load().bm_split_range(lower, upper, sh, n, lo, hi), "bm_split_range")
+    return [(a, b) if a <= b else None for a, b in zip(lo, hi)]
 
 
 def rccl_unique_id() -> bytes:
@@ -251,6 +264,25 @@ class Context:
 
     def set_blocks_per_cu(self, n: int):
         check(self._lib.bm_ctx_set_blocks_per_cu(self.handle, n), "bm_ctx_set_blocks_per_cu")
+
+    def set_split(self, shares):
+        """Integer shares, one per slot (devices, or ranks of the group; the
+        same on every rank), for the range partitioner; None: near-equal."""
+        shares = list(shares or [])
+        arr = (ctypes.c_uint32 * max(len(shares), 1))(*shares)
+        check(self._lib.bm_ctx_set_split(self.handle, arr, len(shares)), "bm_ctx_set_split")
+
+    def get_split(self):
+        """The shares the next search will use ([] when near-equal)."""
+        n = ctypes.c_int(0)
+        check(self._lib.bm_ctx_get_split(self.handle, None, 0, ctypes.byref(n)), "bm_ctx_get_split")
+        arr = (ctypes.c_uint32 * max(n.value, 1))()
+        check(self._lib.bm_ctx_get_split(self.handle, arr, n.value, ctypes.byref(n)), "bm_ctx_get_split")
+        return list(arr[: n.value])
+
+    def set_balance(self, on: bool):
+        """Multi-device contexts: shares follow each device's measured rate."""
+        check(self._lib.bm_ctx_set_balance(self.handle, 1 if on else 0), "bm_ctx_set_balance")
 
     def last_stats(self):
         s = Stats()

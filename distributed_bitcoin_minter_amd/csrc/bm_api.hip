@@ -37,6 +37,11 @@ constexpr int kEventPairs = BM_MAX_LAUNCH_STATS;
 constexpr int kMaxStreams = 4;
 constexpr uint64_t kMaxTailNonces = 1ull << 40;
 constexpr size_t kCtrStride = 32;  // u64 words per launch: counter [0], clock stamps [16..19] (kClockSlot)
+// Balance (bm_ctx_set_balance): a device's rate is measured only when its
+// piece held at least this many nonces (about 20 ms of one MI355X), and the
+// shares are the rates scaled so the fastest device gets kShareScale.
+constexpr uint64_t kBalanceMinNonces = 1ull << 30;
+constexpr double kShareScale = 65536.0;
 
 struct DeviceCtx {
     int id = -1;
@@ -58,6 +63,8 @@ struct DeviceCtx {
     hipEvent_t ev[2 * kEventPairs] = {};
     hipStream_t aux[kMaxStreams - 1] = {};  // extra launch streams (ctx->streams > 1)
     hipEvent_t fork = nullptr, join[kMaxStreams - 1] = {};
+    hipEvent_t bal[2] = {};     // balance: the device's first op and its reduction (timing events)
+    uint64_t piece_nonces = 0;  // nonces of the device's piece in the last call
     ncclComm_t comm = nullptr;  // multi-device ctx: ncclCommInitAll; rank ctx: the process group's
     std::vector<std::pair<const void*, int>> occ;  // kernel -> blocks per CU
     double wall_clock_hz = 100e6;                  // s_memrealtime rate
@@ -106,6 +113,8 @@ struct bm_ctx {
     int rank = 0, world = 1;  // bm_ctx_create_rank: this process's place in an RCCL process group
     int fault_after = -1;     // test hook: fail after enqueueing this many launches (-1: off)
     uint64_t lane_chunk = bm::kNoncesPerLaneChunk;  // nonces per lane per dequeue, at most (BTCMINER_CHUNK)
+    std::vector<uint32_t> shares;  // the partitioner's shares per slot (empty: near-equal pieces)
+    bool balance = false;          // multi-device: shares follow each device's measured rate
     bm_stats_t stats;
 };
 
@@ -239,6 +248,7 @@ int init_device(DeviceCtx& d, int id, int nslots) {
     for (auto& s : d.aux) BM_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     BM_HIP(hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
     for (auto& e : d.join) BM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : d.bal) BM_HIP(hipEventCreate(&e));
     int rc = ensure_counters(d, 256);
     if (rc != BM_OK) return rc;
     return ensure_partials(d, 4096);
@@ -262,6 +272,8 @@ void destroy_device(DeviceCtx& d) {
     if (d.d_test) (void)hipFree(d.d_test);
     if (d.h_result) (void)hipHostFree(d.h_result);
     for (auto& e : d.join)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : d.bal)
         if (e) (void)hipEventDestroy(e);
     if (d.fork) (void)hipEventDestroy(d.fork);
     for (auto& s : d.aux)
@@ -318,6 +330,7 @@ int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches,
         if (!launches[di].empty())
             BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches[di].size() * kCtrStride * sizeof(unsigned long long),
                                   d.stream));
+        if (ctx->balance) BM_HIP(hipEventRecord(d.bal[0], d.stream));
         // stream of each launch: biggest first, round-robin over the streams
         const int ns = std::max(1, std::min<int>(ctx->streams, (int)launches[di].size()));
         std::vector<uint32_t> order(launches[di].size());
@@ -351,6 +364,7 @@ int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches,
         // nparts = 0 (a device or rank with nothing to scan) writes (2^64-1, 2^64-1)
         reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, d.d_result);
         BM_HIP(hipGetLastError());
+        if (ctx->balance) BM_HIP(hipEventRecord(d.bal[1], d.stream));
         if (BM_CLOCK_PROBE && ctx->timing && !launches[di].empty())  // clock stamps, for the launch stats
             BM_HIP(hipMemcpyAsync(d.h_ctr, d.d_ctr, launches[di].size() * kCtrStride * sizeof(unsigned long long),
                                   hipMemcpyDeviceToHost, d.stream));
@@ -420,22 +434,22 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
     // 1. this process's piece (rank contexts: every rank passes the same
     // range and scans its contiguous share of it), split over the devices;
     // plan and size every launch
+    // (the partitioner: slot_pieces over ctx->shares; an empty piece has lo > hi)
     uint64_t lo = lower, hi = upper;
     bool have = true;
     if (ctx->world > 1) {
-        const std::vector<Piece> rp = split_range(lower, upper, ctx->world);
-        if (ctx->rank < (int)rp.size()) {
-            lo = rp[ctx->rank].lo;
-            hi = rp[ctx->rank].hi;
-        } else {
-            have = false;  // a range shorter than the group: nothing here
-        }
+        const Piece mine = slot_pieces(lower, upper, ctx->world, ctx->shares)[(size_t)ctx->rank];
+        lo = mine.lo;
+        hi = mine.hi;
+        have = lo <= hi;  // else a range shorter than the group (or a tiny share): nothing here
     }
     if (have) st.nonces = hi - lo + 1;  // wraps to 0 only for the full 2^64 range
-    const std::vector<Piece> pieces = have ? split_range(lo, hi, ndev) : std::vector<Piece>();
+    const std::vector<Piece> pieces =
+        slot_pieces(have ? lo : 1, have ? hi : 0, ndev, ctx->world > 1 ? std::vector<uint32_t>() : ctx->shares);
     std::vector<std::vector<Launch>> launches(ndev);
     for (int di = 0; di < ndev; ++di) {
-        if (di >= (int)pieces.size()) continue;
+        ctx->devs[di].piece_nonces = pieces[di].lo <= pieces[di].hi ? pieces[di].hi - pieces[di].lo + 1 : 0;
+        if (pieces[di].lo > pieces[di].hi) continue;
         std::vector<bm_segment_t> segs;
         int rc = plan_segments(msg, len, pieces[di].lo, pieces[di].hi, segs, ctx->max_windows);
         if (rc != BM_OK) return rc;
@@ -482,7 +496,26 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         return rc;
     }
 
-    // 4. statistics
+    // 4. balance: the next call's shares follow each device's measured rate
+    if (ctx->balance && ndev > 1) {
+        std::vector<double> rate(ndev, 0.0);
+        bool ok = true;
+        for (int di = 0; di < ndev && ok; ++di) {
+            DeviceCtx& d = ctx->devs[di];
+            float ms = 0.f;
+            ok = d.piece_nonces >= kBalanceMinNonces && hipSetDevice(d.id) == hipSuccess &&
+                 hipEventElapsedTime(&ms, d.bal[0], d.bal[1]) == hipSuccess && ms > 0.f;
+            if (ok) rate[di] = (double)d.piece_nonces / ms;
+        }
+        if (ok) {
+            const double top = *std::max_element(rate.begin(), rate.end());
+            ctx->shares.assign(ndev, 1);
+            for (int di = 0; di < ndev; ++di)
+                ctx->shares[di] = (uint32_t)std::max(1.0, std::floor(rate[di] / top * kShareScale + 0.5));
+        }
+    }
+
+    // 5. statistics
     for (int di = 0; di < ndev; ++di) {
         DeviceCtx& d = ctx->devs[di];
         uint32_t li = 0;
@@ -808,6 +841,51 @@ int bm_ctx_set_task_digits(bm_ctx_t* ctx, int digits) {
 int bm_ctx_set_max_windows(bm_ctx_t* ctx, int max_windows) {
     if (!ctx || max_windows < 0) return BM_EINVAL;
     ctx->max_windows = max_windows;
+    return BM_OK;
+}
+
+int bm_ctx_set_split(bm_ctx_t* ctx, const uint32_t* shares, int n) {
+    if (!ctx || n < 0 || (n > 0 && !shares)) return BM_EINVAL;
+    if (n == 0) {
+        ctx->shares.clear();
+        return BM_OK;
+    }
+    const int slots = ctx->world > 1 ? ctx->world : (int)ctx->devs.size();
+    if (n != slots) return BM_EINVAL;
+    for (int i = 0; i < n; ++i)
+        if (shares[i] == 0) return BM_EINVAL;
+    ctx->shares.assign(shares, shares + n);
+    return BM_OK;
+}
+
+int bm_ctx_get_split(const bm_ctx_t* ctx, uint32_t* shares, int cap, int* n) {
+    if (!ctx || !n || cap < 0 || (cap > 0 && !shares)) return BM_EINVAL;
+    *n = (int)ctx->shares.size();
+    for (int i = 0; i < cap && i < *n; ++i) shares[i] = ctx->shares[(size_t)i];
+    return BM_OK;
+}
+
+int bm_ctx_set_balance(bm_ctx_t* ctx, int enable) {
+    // a rank sees only its own device: a group's shares need an exchange,
+    // which is the caller's (the same bm_ctx_set_split on every rank)
+    if (!ctx || (ctx->world > 1 && enable)) return BM_EINVAL;
+    ctx->balance = enable != 0;
+    return BM_OK;
+}
+
+int bm_split_range(uint64_t lower, uint64_t upper, const uint32_t* shares, int n, uint64_t* lo, uint64_t* hi) {
+    if (n < 1 || n > BM_MAX_SLOTS || !lo || !hi) return BM_EINVAL;
+    std::vector<uint32_t> sh;
+    if (shares) {
+        for (int i = 0; i < n; ++i)
+            if (shares[i] == 0) return BM_EINVAL;
+        sh.assign(shares, shares + n);
+    }
+    const std::vector<bm::Piece> p = bm::slot_pieces(lower, upper, n, sh);
+    for (int i = 0; i < n; ++i) {
+        lo[i] = p[(size_t)i].lo;
+        hi[i] = p[(size_t)i].hi;
+    }
     return BM_OK;
 }
 

@@ -174,4 +174,26 @@ std::vector<Piece> split_range(uint64_t lower, uint64_t upper, int n) {
     return out;
 }
 
+std::vector<Piece> slot_pieces(uint64_t lower, uint64_t upper, int n, const std::vector<uint32_t>& shares) {
+    const Piece empty{1, 0};
+    if (n < 1) return {};
+    if (shares.size() != (size_t)n || lower > upper) {
+        std::vector<Piece> out = split_range(lower, upper, n);
+        out.resize((size_t)n, empty);
+        return out;
+    }
+    std::vector<Piece> out((size_t)n, empty);
+    unsigned __int128 total = 0;
+    for (int i = 0; i < n; ++i) total += shares[(size_t)i];
+    const unsigned __int128 count = (unsigned __int128)(upper - lower) + 1;  // up to 2^64
+    unsigned __int128 prefix = 0, b0 = 0;
+    for (int i = 0; i < n; ++i) {
+        prefix += shares[(size_t)i];
+        const unsigned __int128 b1 = (i == n - 1) ? count : count * prefix / total;
+        if (b1 > b0) out[(size_t)i] = Piece{lower + (uint64_t)b0, lower + (uint64_t)(b1 - 1)};
+        b0 = b1;
+    }
+    return out;
+}
+
 }  // namespace bm

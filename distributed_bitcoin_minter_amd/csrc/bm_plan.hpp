@@ -37,4 +37,13 @@ struct Piece {
 };
 std::vector<Piece> split_range(uint64_t lower, uint64_t upper, int n);
 
+// The multi-GPU range partitioner: one contiguous piece per slot (device or
+// rank), exactly n pieces.  shares empty (or not n of them): split_range's
+// near-equal pieces, padded with empty ones.  Else (every share >= 1) piece
+// i holds the nonces [lower + B_i, lower + B_{i+1} - 1], B_i = floor(count *
+// (s_0 + ... + s_{i-1}) / S) with S the sum of the shares: sizes in
+// proportion to the shares, computed in 128-bit integers so every slot of a
+// process group derives the same pieces.  An empty piece has lo > hi.
+std::vector<Piece> slot_pieces(uint64_t lower, uint64_t upper, int n, const std::vector<uint32_t>& shares);
+
 }  // namespace bm

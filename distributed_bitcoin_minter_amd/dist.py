@@ -10,6 +10,8 @@ same split is done by a multi-device bm_ctx with an RCCL allgather
 the gather runs over xGMI.  bench.py's torchrun ranks use the library's own
 RCCL group instead (bm_ctx_create_rank, rendezvous.py), with no torch.
 """
+import math
+
 U64_MAX = (1 << 64) - 1
 
 
@@ -30,6 +32,36 @@ def split_range(lower: int, upper: int, n: int):
     return out
 
 
+SHARE_SCALE = 65536  # the fastest slot's share (bm_api.hip kShareScale)
+
+
+def slot_pieces(lower: int, upper: int, n: int, shares=None):
+    """Exactly n inclusive pieces, None for an empty one; mirrors
+    bm::slot_pieces (csrc/bm_plan.cpp), the library's partitioner.  shares
+    None (or not n of them): split_range's near-equal pieces.  Else piece i
+    holds [lower + B_i, lower + B_{i+1} - 1], B_i = count * (s_0 + ... +
+    s_{i-1}) // sum(shares)."""
+    if shares is None or len(shares) != n or lower > upper:
+        p = split_range(lower, upper, n)
+        return p + [None] * (n - len(p))
+    count, total = upper - lower + 1, sum(shares)
+    out, prefix, b0 = [], 0, 0
+    for i, sh in enumerate(shares):
+        prefix += sh
+        b1 = count if i == n - 1 else count * prefix // total
+        out.append((lower + b0, lower + b1 - 1) if b1 > b0 else None)
+        b0 = b1
+    return out
+
+
+def shares_from_rates(rates):
+    """Integer shares in proportion to measured rates (nonces per ms), the
+    fastest slot getting SHARE_SCALE; the formula bm_ctx_set_balance uses, so
+    every rank that gathered the same rates derives the same shares."""
+    top = max(rates)
+    return [max(1, math.floor(r / top * SHARE_SCALE + 0.5)) for r in rates]
+
+
 def lex_min(pairs):
     """Lexicographic (hash, nonce) min; (2^64-1, 2^64-1) for no pairs."""
     best = (U64_MAX, U64_MAX)
@@ -39,10 +71,10 @@ def lex_min(pairs):
     return best
 
 
-def rank_piece(lower: int, upper: int, rank: int, world: int):
-    """This rank's inclusive piece, or None if the range is shorter than world."""
-    pieces = split_range(lower, upper, world)
-    return pieces[rank] if rank < len(pieces) else None
+def rank_piece(lower: int, upper: int, rank: int, world: int, shares=None):
+    """This rank's inclusive piece, or None if it is empty (a range shorter
+    than world, or a tiny share)."""
+    return slot_pieces(lower, upper, world, shares)[rank]
 
 
 def combine(partial, device=None):

@@ -27,6 +27,8 @@ class Miner:
 
     def __init__(self, devices=None, num_gpus=1, exclusive_upper=False):
         self.ctx = _lib.Context(devices=devices, num_gpus=num_gpus)
+        if self.ctx.num_devices() > 1:
+            self.ctx.set_balance(True)  # pieces follow each GPU's measured rate (bm_ctx_set_balance)
         self.exclusive_upper = exclusive_upper
 
     def close(self):

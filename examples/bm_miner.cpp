@@ -49,7 +49,9 @@ std::optional<bitcoin::Message> answer(btcminer::Context& ctx, const bitcoin::Me
 }
 
 btcminer::Context open_context(const Options& o) {
-    return o.device >= 0 ? btcminer::Context(std::vector<int>{o.device}) : btcminer::Context(o.gpus);
+    btcminer::Context ctx = o.device >= 0 ? btcminer::Context(std::vector<int>{o.device}) : btcminer::Context(o.gpus);
+    if (ctx.num_devices() > 1) ctx.set_balance(true);  // pieces follow each GPU's measured rate
+    return ctx;
 }
 
 int run_stdin(const Options& o) {

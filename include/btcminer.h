@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BM_ABI_VERSION 3
+#define BM_ABI_VERSION 4
 
 /* status codes */
 #define BM_OK 0
@@ -88,7 +88,8 @@ int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out);
  * then calls bm_ctx_create_rank() on its own device, which blocks until the
  * whole group has joined (ncclCommInitRank).  After that every rank calls
  * bm_search_gpu() with the SAME (msg, lower, upper): rank r scans the r-th
- * of `world` contiguous near-equal pieces of the range, and one RCCL
+ * of `world` contiguous pieces of the range (near-equal, or per
+ * bm_ctx_set_split), and one RCCL
  * allgather of the 16-byte partials gives every rank the result for the
  * whole range.  The reference's equivalent is the server handing each miner
  * a piece of the request (bitcoin/server/server.go:153-169). */
@@ -172,6 +173,34 @@ int bm_ctx_set_task_digits(bm_ctx_t* ctx, int digits);
 #define BM_COMBINE_RCCL 1
 #define BM_COMBINE_HOST 2
 int bm_ctx_set_combine(bm_ctx_t* ctx, int mode);
+
+/* ---- the multi-GPU range partitioner (results never depend on it) -----
+ * A search's range is cut into one contiguous piece per slot: the devices of
+ * a context, or the ranks of an RCCL group.  Default: near-equal pieces.
+ * GPUs run this kernel at different clocks (PMC put it at 2.09-2.23 GHz on
+ * the MI355Xs measured), and a search ends when its slowest slot does;
+ * pieces in proportion to each slot's speed end together.
+ *
+ * bm_ctx_set_split: n integer shares, one per slot (n = devices of the
+ *   context, or world of a rank context), each >= 1; slot i gets the nonces
+ *   [lower + B_i, lower + B_{i+1} - 1] with B_i = floor(count * (s_0 + ... +
+ *   s_{i-1}) / S), S = sum of the shares (exact integer arithmetic, so every
+ *   rank of a group derives the same pieces from the same shares).  Every
+ *   rank of a group must set the same shares.  n = 0: back to near-equal.
+ * bm_ctx_set_balance: a multi-device context sets its own shares after each
+ *   search in which every device's piece held >= 2^30 nonces: each device's
+ *   nonces over the time from its first operation to its reduction, scaled so
+ *   the fastest device has 65536.  BM_EINVAL on a rank context of more than
+ *   one rank: a rank sees only its own device, so a group exchanges its rates
+ *   itself and calls bm_ctx_set_split (bench.py does, over its rendezvous).
+ * bm_ctx_get_split: the shares the next search will use (*n = 0: near-equal).
+ * bm_split_range: the pieces themselves, pure CPU: lo[i] > hi[i] marks an
+ *   empty piece; shares = NULL gives the near-equal pieces. */
+#define BM_MAX_SLOTS 1024
+int bm_ctx_set_split(bm_ctx_t* ctx, const uint32_t* shares, int n);
+int bm_ctx_get_split(const bm_ctx_t* ctx, uint32_t* shares, int cap, int* n);
+int bm_ctx_set_balance(bm_ctx_t* ctx, int enable);
+int bm_split_range(uint64_t lower, uint64_t upper, const uint32_t* shares, int n, uint64_t* lo, uint64_t* hi);
 
 /* ---- test entries (do not change search results) ---------------------- */
 

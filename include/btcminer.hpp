@@ -96,6 +96,12 @@ class Context {
         check(bm_ctx_num_devices(ctx_, &n), "bm_ctx_num_devices");
         return n;
     }
+    // the range partitioner: shares per slot (empty: near-equal), or shares
+    // that follow each device's measured rate (multi-device contexts)
+    void set_split(const std::vector<uint32_t>& shares) {
+        check(bm_ctx_set_split(ctx_, shares.data(), (int)shares.size()), "bm_ctx_set_split");
+    }
+    void set_balance(bool on) { check(bm_ctx_set_balance(ctx_, on ? 1 : 0), "bm_ctx_set_balance"); }
     bm_ctx_t* get() const { return ctx_; }
 
    private:

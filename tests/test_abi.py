@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     lib = _lib.load()
-    assert lib.bm_abi_version() == _lib.BM_ABI_VERSION == 3
+    assert lib.bm_abi_version() == _lib.BM_ABI_VERSION == 4
     for code in range(0, -7, -1):
         assert lib.bm_strerror(code).decode() != "unknown status"
     assert lib.bm_strerror(-99).decode() == "unknown status"

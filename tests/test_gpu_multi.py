@@ -302,3 +302,72 @@ def test_rank_group_bootstrap_two_ranks_one_gpu():
         assert p.returncode == 0, e[-3000:]
         outs.append(json.loads(o.strip().splitlines()[-1]))
     assert all(o["seen"] == [BM_ERCCL, BM_ERCCL] for o in outs), outs
+
+
+def test_weighted_device_split_on_one_gpu(oracle):
+    """The range partitioner with explicit shares (bm_ctx_set_split): three
+    device slots on GPU 0 with shares 1:2:5 scan exactly the pieces
+    bm_split_range cuts, and every answer equals the oracle's."""
+    from distributed_bitcoin_minter_amd import _lib
+    msg, shares = b"bradfitz", [1, 2, 5]
+    with Context(devices=[0, 0, 0]) as c:
+        c.set_split(shares)
+        assert c.get_split() == shares
+        c.set_timing(True)
+        for lo, hi in [(0, 9999), (999_999_000, 1_000_001_000), (U64 - 5000, U64), (7, 9), (10 ** 12 - 4000,
+                                                                                           10 ** 12 + 4000)]:
+            assert c.search(msg, lo, hi) == oracle.search(msg, lo, hi, threads=8), (lo, hi)
+            st = c.last_stats()
+            per = {}
+            for i in range(st.recorded):
+                per[st.launch[i].device] = per.get(st.launch[i].device, 0) + st.launch[i].nonces
+            want = [0 if p is None else p[1] - p[0] + 1 for p in _lib.split_range(lo, hi, 3, shares)]
+            assert [per.get(i, 0) for i in range(3)] == want, (lo, hi)
+        assert c.search(msg, C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
+        for bad in ([1, 2], [1, 0, 1]):
+            with pytest.raises(BtcMinerError) as ei:
+                c.set_split(bad)
+            assert ei.value.status == BM_EINVAL
+        c.set_split(None)
+        assert c.get_split() == []
+
+
+def test_balance_on_one_gpu():
+    """bm_ctx_set_balance: after a search with >= 2^30 nonces per device the
+    context's shares follow each device's measured rate (two slots on one GPU:
+    about equal), the next search splits by them, and both answer C2 right;
+    a small search leaves the shares alone."""
+    msg = bytes.fromhex(C2["msg_hex"])
+    with Context(devices=[0, 0]) as c:
+        c.set_balance(True)
+        assert c.get_split() == []
+        assert c.search(msg, C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
+        sh = c.get_split()
+        assert len(sh) == 2 and max(sh) == 65536 and min(sh) > 0.7 * 65536, sh
+        assert c.search(msg, C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
+        sh2 = c.get_split()
+        assert c.search(b"bradfitz", 0, 9999) == (1419516646206828, 9898)
+        assert c.get_split() == sh2
+
+
+def test_rank_context_split_world1():
+    with Context(devices=[0], rank=0, world=1, unique_id=rccl_unique_id()) as c:
+        c.set_split([3])
+        assert c.search(b"msg", 0, 2) == (4754799531757243342, 1)
+        with pytest.raises(BtcMinerError):
+            c.set_split([1, 1])  # one share per rank
+
+
+def test_bench_rehearsals_balance_after_warmup():
+    """bench.py's range partitioner, rehearsed on one GPU: after one warmup
+    step the one-process 2-way split balances itself (bm_ctx_set_balance),
+    and 2 torchrun ranks exchange their measured rates over the rendezvous
+    and cut by the shares (dist.rank_piece); both answers equal the weak2
+    golden."""
+    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--rehearse-one-gpu"]))
+    sp = out["config"]["split"]
+    assert out["result_ok"] is True and sp["mode"].startswith("measured device rates") and len(sp["shares"]) == 2
+    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "1", "--rehearse-one-gpu"], torchrun=2))
+    sp = out["config"]["split"]
+    assert out["result_ok"] is True and sp["mode"].startswith("measured rank rates"), sp
+    assert len(sp["shares"]) == 2 and max(sp["shares"]) == 65536
