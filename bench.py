@@ -63,7 +63,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from distributed_bitcoin_minter_amd import _lib  # noqa: E402
-from distributed_bitcoin_minter_amd._lib import Context, device_count, rccl_unique_id  # noqa: E402
+from distributed_bitcoin_minter_amd._lib import Context, device_count, device_pci_bus_id, rccl_unique_id  # noqa: E402
 from distributed_bitcoin_minter_amd.dist import lex_min, rank_piece, shares_from_rates  # noqa: E402
 
 U64 = (1 << 64) - 1
@@ -151,6 +151,49 @@ def issue_bound(p, nbv, clock_ghz):
     return {"valu_per_nonce": lay["valu"], "slow": lay["valu_slow"], "fast": lay["valu_fast"],
             "issue_slots_per_nonce": lay["issue_slots"], "clock_ghz": round(clock_ghz, 3),
             "GHs_per_gpu": round(ghs, 2)}
+
+
+class ClockSampler:
+    """The driver's gfx clock of one GPU (hwmon freq1_input, found through
+    the device's PCI bus id) sampled every `period` s on a host thread while
+    the timed region runs, with no change to the kernels.  It tracks the PMC
+    clock to about 1% (it reads high: 2.235-2.241 GHz against 2.20-2.22 by
+    PMC on one box, profiles/r02/s2_clock_sources.log), so it is reported
+    beside the issue bound, and per rank at N > 1, not used for it.  Silent
+    (None) where sysfs does not expose it."""
+
+    def __init__(self, device, period=0.05):
+        import threading
+        self.period, self.samples, self.path = period, [], None
+        try:
+            bus = device_pci_bus_id(device).lower()
+            paths = sorted(glob.glob(f"/sys/bus/pci/devices/{bus}/hwmon/hwmon*/freq1_input"))
+            self.path = paths[0] if paths else None
+        except Exception:  # noqa: BLE001 -- informational only
+            self.path = None
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, daemon=True) if self.path else None
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                with open(self.path) as f:
+                    self.samples.append(int(f.read()))
+            except (OSError, ValueError):
+                return
+            self._stop.wait(self.period)
+
+    def start(self):
+        if self._thread:
+            self._thread.start()
+
+    def stop(self):
+        """Mean clock in GHz over the samples, or None."""
+        if not self._thread:
+            return None
+        self._stop.set()
+        self._thread.join()
+        return sum(self.samples) / len(self.samples) / 1e9 if self.samples else None
 
 
 def hip_runtimes():
@@ -415,7 +458,9 @@ def main():
     for _ in range(args.warmup):
         step()
     split = calibrate_split(args, ctx, grp)
+    sampler = ClockSampler(0 if args.rehearse_one_gpu else (local if world > 1 else 0))
     grp.barrier()
+    sampler.start()
     t0 = time.perf_counter()
     doms = []
     res = None
@@ -423,8 +468,10 @@ def main():
         res, d = step()
         doms.append(d)
     dt = time.perf_counter() - t0
+    sysfs_clock = sampler.stop()
     grp.barrier()
     dt = grp.max(dt)
+    clocks = grp.gather(sysfs_clock) if world > 1 else [sysfs_clock]
 
     total = hi - lo + 1
     value = total * args.steps / dt / 1e9
@@ -493,6 +540,11 @@ def main():
         live_clock = sum(live) / len(live) if live else None
         if live_clock:
             roof["clock_ghz_live"] = round(live_clock, 3)
+        if sysfs_clock:
+            # the driver's gfx clock over the timed region: on one box it read
+            # 2.235-2.241 GHz where PMC put the dominant launch at 2.20-2.22
+            # (profiles/r02/s2_clock_sources.log), so it is reported, not used
+            roof["clock_ghz_sysfs"] = round(sysfs_clock, 3)
         ib_clock = live_clock or clock
         if ib_clock:
             ib = issue_bound(dom.p, dom.nbv, ib_clock)
@@ -512,6 +564,10 @@ def main():
             roof["call"] = {"achieved": round(ach, 3), "frac": round(ach / VALU_PEAK_T, 4), "span_ms": round(span, 3),
                             "launches": ctx.last_stats().launches}
         out["roofline"] = roof
+    if world > 1 and any(c is not None for c in clocks):
+        # each rank's GPU clock over the timed region (driver hwmon): what
+        # the range partitioner balances against
+        out["clock_ghz_sysfs_per_rank"] = [None if c is None else round(c, 3) for c in clocks]
     if args.rehearse_one_gpu:
         out["rehearsal"] = "every rank / device is GPU 0: checks the multi-GPU split and combine, not a measurement"
     if grp.rank == 0 and n == 1 and not args.no_cpu_baseline:

@@ -79,6 +79,7 @@ def load():
         "bm_abi_version": ([], ctypes.c_int),
         "bm_strerror": ([ctypes.c_int], ctypes.c_char_p),
         "bm_device_count": ([P(ctypes.c_int)], ctypes.c_int),
+        "bm_device_pci_bus_id": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
         "bm_ctx_create": ([ctypes.c_int, P(vp)], ctypes.c_int),
         "bm_ctx_create_devices": ([P(ctypes.c_int), ctypes.c_int, P(vp)], ctypes.c_int),
         "bm_ctx_destroy": ([vp], ctypes.c_int),
@@ -134,6 +135,13 @@ def device_count():
     n = ctypes.c_int(0)
     check(load().bm_device_count(ctypes.byref(n)), "bm_device_count")
     return n.value
+
+
+def device_pci_bus_id(device: int) -> str:
+    """PCI bus id of a visible device, e.g. "0000:05:00.0"."""
+    buf = ctypes.create_string_buffer(64)
+    check(load().bm_device_pci_bus_id(device, buf, len(buf)), "bm_device_pci_bus_id")
+    return buf.value.decode()
 
 
 DEFAULT_MAX_WINDOWS = 64

@@ -652,6 +652,13 @@ int bm_device_count(int* out) {
     return BM_OK;
 }
 
+int bm_device_pci_bus_id(int device, char* buf, int len) {
+    if (!buf || len < 13) return BM_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return BM_ENODEV;
+    return hipDeviceGetPCIBusId(buf, len, device) == hipSuccess ? BM_OK : BM_EHIP;
+}
+
 }  // extern "C"
 
 namespace bm {

@@ -67,6 +67,9 @@ const char* bm_strerror(int status);
 
 /* Number of visible HIP devices (0 when there is none). */
 int bm_device_count(int* out);
+/* PCI bus id of a visible device ("0000:05:00.0"; len >= 13), e.g. to find
+ * its driver clock in sysfs (bench.py samples it while it times). */
+int bm_device_pci_bus_id(int device, char* buf, int len);
 
 /* Context over devices 0..num_gpus-1 (num_gpus = 0: all visible devices).
  * A context with several devices splits every search across them and
