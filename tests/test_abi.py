@@ -55,6 +55,13 @@ def test_invalid_arguments_rejected():
     assert lib.bm_reduce_gpu(None, None, 0, ctypes.byref(r)) == _lib.BM_EINVAL
     assert lib.bm_ctx_set_test_fault(None, 0) == _lib.BM_EINVAL
     assert lib.bm_ctx_rank(None, ctypes.byref(n), ctypes.byref(n)) == _lib.BM_EINVAL
+    assert lib.bm_ctx_set_split(None, None, 0) == _lib.BM_EINVAL
+    assert lib.bm_ctx_get_split(None, None, 0, ctypes.byref(n)) == _lib.BM_EINVAL
+    assert lib.bm_ctx_set_balance(None, 1) == _lib.BM_EINVAL
+    buf = ctypes.create_string_buffer(64)
+    assert lib.bm_device_pci_bus_id(0, None, 64) == _lib.BM_EINVAL
+    assert lib.bm_device_pci_bus_id(0, buf, 4) == _lib.BM_EINVAL
+    assert lib.bm_device_pci_bus_id(-1, buf, 64) == _lib.BM_ENODEV
 
 
 @pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")
