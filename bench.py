@@ -325,7 +325,8 @@ SPLIT = {"shares": None, "library": False}
 
 
 def calibrate_split(args, ctx, grp):
-    """After the warmup: each GPU's rate in the last warmup step (its own
+    """After the warmup (ranks: at least 2 steps, so the one timed is warm):
+    each GPU's rate in the last warmup step (its own
     nonces over its launches' span, HIP events, so the wait for the other
     ranks does not count) -> integer shares, the same on every rank -> the
     timed steps cut the range in proportion (bm_ctx_set_split).
@@ -333,6 +334,10 @@ def calibrate_split(args, ctx, grp):
     Returns what the bench line reports."""
     if args.no_balance or args.warmup < 1:
         return {"mode": "near-equal"}
+    if grp.world > 1 and args.warmup < 2:
+        # the first call of a process loads each kernel's code object on
+        # first launch, which stretches its span: time a warm call
+        return {"mode": "near-equal", "note": "the ranks calibrate on the second warmup step"}
     if grp.world == 1:
         if ctx.num_devices() == 1:
             return {"mode": "one device"}

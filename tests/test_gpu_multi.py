@@ -361,13 +361,13 @@ def test_rank_context_split_world1():
 def test_bench_rehearsals_balance_after_warmup():
     """bench.py's range partitioner, rehearsed on one GPU: after one warmup
     step the one-process 2-way split balances itself (bm_ctx_set_balance),
-    and 2 torchrun ranks exchange their measured rates over the rendezvous
-    and cut by the shares (dist.rank_piece); both answers equal the weak2
-    golden."""
+    and 2 torchrun ranks exchange the rates of their second (warm) warmup step
+    over the rendezvous and cut by the shares (dist.rank_piece); both
+    answers equal the weak2 golden."""
     out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--rehearse-one-gpu"]))
     sp = out["config"]["split"]
     assert out["result_ok"] is True and sp["mode"].startswith("measured device rates") and len(sp["shares"]) == 2
-    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "1", "--rehearse-one-gpu"], torchrun=2))
+    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "2", "--rehearse-one-gpu"], torchrun=2))
     sp = out["config"]["split"]
     assert out["result_ok"] is True and sp["mode"].startswith("measured rank rates"), sp
     assert len(sp["shares"]) == 2 and max(sp["shares"]) == 65536
