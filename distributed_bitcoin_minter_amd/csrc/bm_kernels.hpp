@@ -309,6 +309,9 @@ BM_DEV uint64_t readfirstlane_u64(uint64_t v) {
 #ifndef BM_FOLD  // sha_rounds_h0's shortcuts in the inner loop (0 = plain rounds, for A/B)
 #define BM_FOLD 1
 #endif
+#ifndef BM_WAVES_MAIN  // waves/SIMD of the 1-block layouts (most of every search)
+#define BM_WAVES_MAIN 7
+#endif
 #ifndef BM_WAVES_PAD
 #define BM_WAVES_PAD 5
 #endif
@@ -316,7 +319,7 @@ BM_DEV uint64_t readfirstlane_u64(uint64_t v) {
 #define BM_WAVES_NBV2 6
 #endif
 constexpr int search_waves(int P, int NBV) {
-    return (NBV == 1 && P >= 55) ? BM_WAVES_PAD : (NBV == 2 ? BM_WAVES_NBV2 : 8);
+    return (NBV == 1 && P >= 55) ? BM_WAVES_PAD : (NBV == 2 ? BM_WAVES_NBV2 : BM_WAVES_MAIN);
 }
 #ifndef BM_LDS_BEST  // a lane's running best (hash, nonce) kept in LDS, not in VGPRs (A/B knob)
 #define BM_LDS_BEST 0
