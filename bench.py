@@ -558,7 +558,7 @@ def main():
                 ib["frac"] = round(dom.nonces / (dom_ms * 1e-3) / 1e9 / ib["GHs_per_gpu"], 4)
                 if not live_clock:
                     ib["note"] = ("clock from the committed PMC profile (another run; boxes run this kernel at "
-                                  "2.12-2.23 GHz), so frac can exceed 1 on a faster box")
+                                  "2.04-2.23 GHz), so frac can exceed 1 on a faster box")
                 roof["issue_bound"] = ib
         if calls:
             # the whole call on this device: every launch's algorithmic ops over
