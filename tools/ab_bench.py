@@ -2,6 +2,7 @@
 """A/B the search kernels of several libbtcminer builds on the GPU.
 
     python tools/ab_bench.py distributed_bitcoin_minter_amd/libbtcminer*.so
+    python tools/ab_bench.py BTCMINER_STREAMS=2 BTCMINER_STREAMS=1,BTCMINER_CHUNK=200
 
 Each library runs in its own process (BTCMINER_LIB): C2 ("bradfitz",
 [0, 2^32-1]) and C3 (120-B msg, [2^64-2^32, 2^64-1]), checked against the
@@ -18,7 +19,7 @@ def one(reps):
     sys.path.insert(0, ROOT)
     from distributed_bitcoin_minter_amd import Context
     gold = {c["config"]: c for c in json.load(open(os.path.join(ROOT, "tests/golden/full_range.json")))["cases"]}
-    out = {"lib": os.path.basename(os.environ.get("BTCMINER_LIB", "default"))}
+    out = {"lib": os.environ.get("AB_TAG") or os.path.basename(os.environ.get("BTCMINER_LIB", "default"))}
     bpc = int(os.environ.get("AB_BPC", "0"))
     with Context(devices=[0]) as ctx:
         ctx.set_timing(True)
@@ -47,8 +48,15 @@ def one(reps):
 def main():
     if os.environ.get("AB_CHILD"):
         return one(int(os.environ.get("AB_REPS", "5")))
-    for lib in sys.argv[1:]:
-        env = dict(os.environ, BTCMINER_LIB=os.path.abspath(lib), AB_CHILD="1")
+    for arg in sys.argv[1:]:
+        # a library path, or KEY=VALUE[,KEY=VALUE...]: the default library
+        # under those environment knobs (BTCMINER_STREAMS, BTCMINER_CHUNK, ...)
+        if "=" in arg:
+            extra = dict(kv.split("=", 1) for kv in arg.split(","))
+            lib = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "libbtcminer.so")
+        else:
+            extra, lib = {}, arg
+        env = dict(os.environ, BTCMINER_LIB=os.path.abspath(lib), AB_CHILD="1", AB_TAG=arg, **extra)
         r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, timeout=300)
         if r.returncode != 0:
             print(json.dumps({"lib": lib, "rc": r.returncode}), flush=True)
