@@ -6,7 +6,11 @@
 
 namespace bm {
 
-constexpr int kBlock = 256;  // threads per workgroup of the search kernels (4 waves)
+#ifndef BM_BLOCK  // threads per workgroup of the search kernels (a build knob for A/B)
+#define BM_BLOCK 256
+#endif
+constexpr int kBlock = BM_BLOCK;  // 4 waves
+static_assert(kBlock % 64 == 0 && kBlock >= 64 && kBlock <= 1024, "whole waves");
 
 struct Partial {  // 16-byte result, ordered lexicographically (hash, nonce)
     uint64_t hash;
