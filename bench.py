@@ -165,6 +165,9 @@ class ClockSampler:
     def __init__(self, device, period=0.05):
         import threading
         self.period, self.samples, self.path = period, [], None
+        if period is None:  # off
+            self._thread = None
+            return
         try:
             bus = device_pci_bus_id(device).lower()
             paths = sorted(glob.glob(f"/sys/bus/pci/devices/{bus}/hwmon/hwmon*/freq1_input"))
@@ -428,6 +431,10 @@ def main():
     ap.add_argument("--combine", default="rccl", choices=["rccl", "gather"],
                     help="torchrun ranks: in-library RCCL allgather (default) or a gather over the rendezvous")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--clock-sample", type=int, default=None,
+                    help="1: sample the driver's gfx clock during the timed region (reported, not used); "
+                         "default: only at N > 1, where each rank's clock explains the scaling "
+                         "(it cost about 0.1%% at N = 1, profiles/r02/s2_sampler_ab.log)")
     ap.add_argument("--no-balance", action="store_true",
                     help="keep near-equal pieces (default: after the warmup, pieces follow each GPU's measured rate)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -463,7 +470,8 @@ def main():
     for _ in range(args.warmup):
         step()
     split = calibrate_split(args, ctx, grp)
-    sampler = ClockSampler(0 if args.rehearse_one_gpu else (local if world > 1 else 0))
+    sampler = ClockSampler(0 if args.rehearse_one_gpu else (local if world > 1 else 0),
+                           period=0.05 if (args.clock_sample if args.clock_sample is not None else n > 1) else None)
     grp.barrier()
     sampler.start()
     t0 = time.perf_counter()
