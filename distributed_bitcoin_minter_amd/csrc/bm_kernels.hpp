@@ -316,10 +316,14 @@ BM_DEV uint64_t readfirstlane_u64(uint64_t v) {
 #define BM_WAVES_PAD 5
 #endif
 #ifndef BM_WAVES_NBV2
-#define BM_WAVES_NBV2 6
+#define BM_WAVES_NBV2 7
 #endif
+// NBV = 2 layouts whose inner loop spills at 7 waves/SIMD (72 VGPRs) keep 6
+// (tools/check_inner.py: 0 layouts with scratch in the inner loop).
+constexpr bool nbv2_tight(int P) { return P == 4 || P == 13 || P == 14; }
 constexpr int search_waves(int P, int NBV) {
-    return (NBV == 1 && P >= 55) ? BM_WAVES_PAD : (NBV == 2 ? BM_WAVES_NBV2 : BM_WAVES_MAIN);
+    return (NBV == 1 && P >= 55) ? BM_WAVES_PAD
+                                 : (NBV == 2 ? (nbv2_tight(P) ? 6 : BM_WAVES_NBV2) : BM_WAVES_MAIN);
 }
 #ifndef BM_LDS_BEST  // a lane's running best (hash, nonce) kept in LDS, not in VGPRs (A/B knob)
 #define BM_LDS_BEST 0

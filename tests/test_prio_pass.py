@@ -336,3 +336,20 @@ def test_drop_dead_smov_keeps_the_inner_loop():
            "\ts_mov_b32 s6, 6\n", ".Lfunc_end0:\n"]
     out, n = bm_prio.drop_dead_smov(blk, ["foo"])
     assert n == 1 and "\ts_mov_b32 s6, 5\n" not in out and len(out) == len(blk) - 1
+
+
+def test_no_inner_loop_spills_in_the_build():
+    """Every search_kernel<P, NBV> of the built library keeps its inner loop
+    free of scratch / memory / lane-spill ops (tools/check_inner.py on the
+    device assembly): the occupancy requests (7 waves/SIMD for the 1-block
+    and most NBV = 2 layouts) must not push the hot loop into spills."""
+    import glob
+    import subprocess
+    import sys
+    build = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc", "build")
+    if not glob.glob(os.path.join(build, "inst*-hip-amdgcn-amd-amdhsa-gfx950.s")):
+        pytest.skip("device assembly not built (make -C distributed_bitcoin_minter_amd/csrc)")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_inner.py"), build], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert "83 kernels checked, 0 with scratch" in r.stdout
