@@ -30,10 +30,21 @@ unaffected (tests/test_prio_pass.py interprets a sample both ways; the GPU
 parity suite runs on the built library).  A toggle goes before the first
 VALU of every run whose class differs from the current priority; the state is
 reset at every label (any block may be entered from elsewhere).
+
+The pass runs after LLVM's hazard recognizer and waitcnt insertion, so its
+output goes through bm_asm_guard.check before it is written: no inserted or
+moved instruction may touch a register an outstanding load targets, a
+rewrite touches only the registers of the instruction it replaces, and no
+pair of the compiler's instructions that needs wait states may end up closer
+than the compiler placed it.  A refused rewrite fails the build (exit 3).
 """
 import argparse
+import os
 import re
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from bm_asm_guard import GuardError, Made, check as guard_check  # noqa: E402
 
 FAST_OPS = {
     "v_add_u32", "v_sub_u32", "v_subrev_u32", "v_xor_b32", "v_or_b32", "v_and_b32", "v_not_b32",
@@ -134,12 +145,12 @@ def fold_sgpr_constants(lines, kernels):
                     if len(ks) == 1 and len(vs) == 2:
                         lit = known(ops[ks[0]])
                         x, y = ops[vs[0]], ops[vs[1]]
-                        out.append(f"\tv_add_u32_e32 {ops[0]}, {x}, {y}\n")
-                        out.append(f"\tv_add_u32_e32 {ops[0]}, {lit}, {ops[0]}\n")
+                        out.append(Made(f"\tv_add_u32_e32 {ops[0]}, {x}, {y}\n", "rewrite", ln))
+                        out.append(Made(f"\tv_add_u32_e32 {ops[0]}, {lit}, {ops[0]}\n", "rewrite", ln))
                         n_split += 1
                         continue
                 elif len(ops) == 3 and known(ops[1]) and VREG_RE.match(ops[2]):
-                    out.append(f"\t{m.group(1)} {ops[0]}, {known(ops[1])}, {ops[2]}\n")
+                    out.append(Made(f"\t{m.group(1)} {ops[0]}, {known(ops[1])}, {ops[2]}\n", "rewrite", ln))
                     n_fold += 1
                     continue
             for r in _sdefs(ln):
@@ -190,16 +201,16 @@ def drop_dead_smov(lines, kernels, replace=None):
         if replace is None:
             del out[i]
         else:
-            out[i] = replace
+            out[i] = Made(replace, "rewrite", lines[i])
         n += 1
     return out, n
 
 
-def space_dependent_valu(lines, kernels):
-    """Insert s_nop 0 between two adjacent VALU ops of the search kernels'
-    big blocks when the second reads what the first wrote (an A/B probe of
-    whether the dead SALU writes the fold leaves behind help by spacing a
-    wave's dependent VALU)."""
+def space_dependent_valu(lines, kernels, spacer="\ts_nop 0\n"):
+    """Insert `spacer` (s_nop 0) between two adjacent VALU ops of the search
+    kernels' big blocks when the second reads what the first wrote (an A/B
+    probe of whether the dead SALU writes the fold leaves behind help by
+    spacing a wave's dependent VALU)."""
     out, in_kernel, prev, n = [], False, None, 0
     for ln in lines:
         m_fn = re.match(r"^(_Z\S+):", ln)
@@ -217,7 +228,7 @@ def space_dependent_valu(lines, kernels):
         mn, defs, uses = du
         if mn.startswith("v_"):
             if prev is not None and prev & uses:
-                out.append("\ts_nop 0\n")
+                out.append(Made(spacer, "insert"))
                 n += 1
             prev = defs
         out.append(ln)
@@ -251,8 +262,8 @@ def split_add3(lines, kernels, every):
                         first = (hits + rest)[:2]   # every read of d happens in the first add
                         last = (hits + rest)[2]
                         if len(hits) <= 2 and last != d:
-                            out.append(f"\tv_add_u32_e32 {d}, {first[0]}, {first[1]}\n")
-                            out.append(f"\tv_add_u32_e32 {d}, {last}, {d}\n")
+                            out.append(Made(f"\tv_add_u32_e32 {d}, {first[0]}, {first[1]}\n", "rewrite", ln))
+                            out.append(Made(f"\tv_add_u32_e32 {d}, {last}, {d}\n", "rewrite", ln))
                             n += 1
                             continue
         out.append(ln)
@@ -351,7 +362,8 @@ def _schedule(seg, max_run):
             if indeg[j] == 0:
                 heapq.heappush(ready, j)
     assert len(order) == n, "dependence cycle"
-    return [seg[i] for i in order]
+    return [seg[i] if k == i else Made(seg[i], "move", seg[i].orig if isinstance(seg[i], Made) else seg[i])
+            for k, i in enumerate(order)]
 
 
 def cluster_runs(lines, kernels, max_run=0, min_valu=64):
@@ -415,7 +427,7 @@ def run(lines, kernels, slow, fast, min_fast_run=1):
                 if run_len < min_fast_run and cur == "S":
                     want = "S"
             if want != cur:
-                out.append(f"\ts_setprio {slow if want == 'S' else fast}\n")
+                out.append(Made(f"\ts_setprio {slow if want == 'S' else fast}\n", "insert"))
                 n_toggle += 1
                 cur = want
         out.append(line)
@@ -451,14 +463,16 @@ def main():
     ap.add_argument("--lead-slow", type=int, default=0, help="1: each s_setprio <slow> one VALU earlier")
     ap.add_argument("--lead-fast", type=int, default=0, help="1: each s_setprio <fast> one VALU earlier")
     ap.add_argument("--space-dependent", type=int, default=0,
-                    help="1: s_nop 0 between adjacent VALU where the second reads the first's result")
+                    help="1: s_nop 0 between adjacent VALU where the second reads the first's result; "
+                         "2: s_mov_b32 s0, s0 there instead (round 2's faulting variant, DESIGN.md §8)")
     ap.add_argument("--split-add3-every", type=int, default=0,
                     help="K > 0: split every K-th all-VGPR v_add3_u32 into two v_add_u32")
     ap.add_argument("--cluster", type=int, default=-1,
                     help=">= 0: reorder big blocks into longer slow / fast runs (0: unbounded runs, "
                          "K: at most K in a row); -1: off")
     a = ap.parse_args()
-    lines = open(a.src).readlines()
+    orig = open(a.src).readlines()
+    lines = list(orig)
     if a.fold_sgpr:
         lines, n_fold, n_split = fold_sgpr_constants(lines, a.kernels.split(","))
         print(f"bm_prio: {a.src}: {n_fold} SGPR constants folded, {n_split} v_add3 split", file=sys.stderr)
@@ -467,8 +481,9 @@ def main():
         print(f"bm_prio: {a.src}: {n_dead} dead s_mov_b32 {'removed' if a.drop_dead_smov == 1 else 'made s_nop 0'}",
               file=sys.stderr)
     if a.space_dependent:
-        lines, n_sp = space_dependent_valu(lines, a.kernels.split(","))
-        print(f"bm_prio: {a.src}: {n_sp} s_nop 0 between dependent VALU", file=sys.stderr)
+        spacer = "\ts_mov_b32 s0, s0\n" if a.space_dependent == 2 else "\ts_nop 0\n"
+        lines, n_sp = space_dependent_valu(lines, a.kernels.split(","), spacer)
+        print(f"bm_prio: {a.src}: {n_sp} `{spacer.strip()}` between dependent VALU", file=sys.stderr)
     if a.split_add3_every:
         lines, n_split3 = split_add3(lines, a.kernels.split(","), a.split_add3_every)
         print(f"bm_prio: {a.src}: {n_split3} all-VGPR v_add3 split", file=sys.stderr)
@@ -479,8 +494,16 @@ def main():
         if on:
             out, n_lead = lead_toggles(out, prio)
             print(f"bm_prio: {a.src}: {n_lead} s_setprio {prio} moved one VALU earlier", file=sys.stderr)
+    # every rewrite checked against the compiler's own assembly (bm_asm_guard.py)
+    try:
+        g = guard_check(orig, out, a.kernels.split(","))
+    except GuardError as e:
+        print(f"bm_prio: {a.src}: REFUSED by the assembly guard: {e}", file=sys.stderr)
+        sys.exit(3)
     open(a.dst, "w").writelines(out)
-    print(f"bm_prio: {a.src}: {n_toggle} s_setprio over {n_valu} VALU", file=sys.stderr)
+    print(f"bm_prio: {a.src}: {n_toggle} s_setprio over {n_valu} VALU; guard: {g['kernels']} kernels, "
+          f"{g['inserted']} inserted, {g['rewritten']} rewritten, {g['moved']} moved, {g['deleted']} deleted, "
+          f"{g['pairs']} padded pairs closer (all interlocked)", file=sys.stderr)
 
 
 if __name__ == "__main__":

@@ -353,3 +353,134 @@ def test_no_inner_loop_spills_in_the_build():
                        text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:]
     assert "83 kernels checked, 0 with scratch" in r.stdout
+
+
+# ---- the assembly guard (csrc/bm_asm_guard.py) -------------------------------
+
+import bm_asm_guard as guard  # noqa: E402
+
+BUILD = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc", "build")
+
+
+def _passes(lines, spacer=None, drop=0, cluster=-1):
+    """bm_prio's pipeline as main() runs it (fold, options, toggles)."""
+    ks = ["search_kernel"]
+    out, _, _ = bm_prio.fold_sgpr_constants(list(lines), ks)
+    if drop:
+        out, _ = bm_prio.drop_dead_smov(out, ks, "\ts_nop 0\n" if drop == 2 else None)
+    if spacer:
+        out, _ = bm_prio.space_dependent_valu(out, ks, spacer)
+    if cluster >= 0:
+        out = bm_prio.cluster_runs(out, ks, max_run=cluster)
+    out, _, _ = bm_prio.run(out, ks, 2, 0)
+    return out
+
+
+SMEM_KERNEL = """\
+_ZN2bm13search_kernelILi16ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
+\ts_load_dwordx4 s[0:3], s[12:13], 0x1e0
+\tv_mov_b32_e32 v2, s25
+\tv_bitop3_b32 v2, s24, v2, v3 bitop3:0xca
+\tv_alignbit_b32 v3, s20, s20, 2
+\ts_waitcnt lgkmcnt(0)
+\tv_mov_b32_e32 v4, s0
+\tv_add_u32_e32 v5, v4, v2
+\tglobal_store_dwordx4 v12, v[0:3], s[0:1]
+\ts_endpgm
+.Lfunc_end5:
+"""
+
+
+def test_guard_refuses_a_write_racing_an_outstanding_smem_load():
+    """Round 2's faulting variant: `s_mov_b32 s0, s0` between
+    dependent VALU landed while `s_load_dwordx4 s[0:3]` (the partials and
+    counter pointers) was still outstanding in search_kernel<16, 1> of the
+    8-wave build.  The self-move reads the stale s0 and writes it back, so a
+    load landing in between loses its low half.  The guard refuses it; the
+    same spacer after the wait, and the s_nop spacer, pass."""
+    orig = SMEM_KERNEL.splitlines(keepends=True)
+    bad = _passes(orig, spacer="\ts_mov_b32 s0, s0\n")
+    assert "\ts_mov_b32 s0, s0\n" in bad
+    with pytest.raises(guard.GuardError, match=r"s_mov_b32 s0, s0.*\['s0'\].*outstanding"):
+        guard.check(orig, bad, ["search_kernel"])
+    guard.check(orig, _passes(orig, spacer="\ts_nop 0\n"), ["search_kernel"])
+    # the same instruction inserted after the wait is fine
+    late = list(orig)
+    late.insert(6, guard.Made("\ts_mov_b32 s0, s0\n", "insert"))
+    guard.check(orig, late, ["search_kernel"])
+
+
+def test_guard_counter_model():
+    """LDS returns in order within lgkmcnt, SMEM out of order (only
+    lgkmcnt(0) retires it), VMEM in order within vmcnt; a join keeps what
+    either path left pending."""
+    k = """\
+_ZN2bm13search_kernelILi3ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
+\ts_load_dword s4, s[0:1], 0x0
+\tds_read_b32 v1, v0
+\tds_read_b32 v2, v0 offset:4
+\ts_waitcnt lgkmcnt(1)
+\tv_add_u32_e32 v9, v9, v9
+\tscratch_load_dword v3, off, off
+\tscratch_load_dword v4, off, off offset:4
+\ts_waitcnt vmcnt(1)
+\ts_cbranch_scc1 .LBB0_2
+\tds_read_b32 v5, v0
+.LBB0_2:
+\tv_add_u32_e32 v8, v8, v8
+\ts_endpgm
+.Lfunc_end0:
+"""
+    lines = k.splitlines(keepends=True)
+    _, lo, hi = guard.kernel_ranges(lines, ["search_kernel"])[0]
+    before, _ = guard.pending_states(lines, lo, hi)
+    at = lambda text: {r for r, _c in before[next(i for i in range(lo, hi) if lines[i].strip() == text)]}
+    p = at("v_add_u32_e32 v9, v9, v9")
+    assert "v1" not in p and "v2" in p and "s4" in p      # lgkmcnt(1): the older LDS read is done, SMEM is not
+    p = at("v_add_u32_e32 v8, v8, v8")
+    assert "v3" not in p and "v4" in p and "v5" in p      # vmcnt(1) retires v3; v5 pending on the fall-through path
+
+
+def test_guard_refuses_shrinking_a_padded_pair_and_foreign_rewrites():
+    """Deleting an instruction between a VALU write of v1 and a DPP read of it
+    (which the hardware does not interlock) shortens what the compiler padded;
+    a rewrite that reads a register its original did not is refused too."""
+    k = """\
+_ZN2bm13search_kernelILi3ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
+\tv_add_u32_e32 v1, v2, v3
+\ts_mov_b32 s4, 1
+\ts_mov_b32 s4, 2
+\tv_mov_b32_dpp v2, v1 row_shr:1 row_mask:0xf bank_mask:0xf
+\tv_add_u32_e32 v6, s4, v6
+\ts_endpgm
+.Lfunc_end0:
+"""
+    orig = k.splitlines(keepends=True)
+    dropped, n = bm_prio.drop_dead_smov(list(orig), ["search_kernel"])
+    assert n == 1
+    with pytest.raises(guard.GuardError, match="v_mov_b32_dpp"):
+        guard.check(orig, dropped, ["search_kernel"])
+    noped, _ = bm_prio.drop_dead_smov(list(orig), ["search_kernel"], "\ts_nop 0\n")
+    guard.check(orig, noped, ["search_kernel"])          # same slot count: accepted
+    foreign = list(orig)
+    foreign[5] = guard.Made("\tv_add_u32_e32 v6, v7, v6\n", "rewrite", orig[5])
+    with pytest.raises(guard.GuardError, match="touches other registers"):
+        guard.check(orig, foreign, ["search_kernel"])
+
+
+@pytest.mark.parametrize("name", ["inst1_16_23", "inst1_56_63"])
+def test_guard_on_the_built_assembly(name):
+    """The shipped pipeline passes the guard on the real device assembly
+    (the build runs the same check and fails on a violation); the s0 spacer
+    variant is refused on the padding-block layouts, whose compiler code
+    keeps `s_load_dwordx4 s[0:3]` outstanding across VALU rounds."""
+    src = os.path.join(BUILD, f"{name}.dev.s")
+    if not os.path.exists(src):
+        pytest.skip("device assembly not built (make -C distributed_bitcoin_minter_amd/csrc)")
+    orig = open(src).readlines()
+    st = guard.check(orig, _passes(orig), ["search_kernel"])
+    assert st["kernels"] == 8 and st["inserted"] > 1000 and st["rewritten"] > 0 and st["deleted"] == 0
+    guard.check(orig, _passes(orig, drop=2), ["search_kernel"])
+    if name == "inst1_56_63":
+        with pytest.raises(guard.GuardError, match="outstanding"):
+            guard.check(orig, _passes(orig, spacer="\ts_mov_b32 s0, s0\n"), ["search_kernel"])
