@@ -63,8 +63,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from distributed_bitcoin_minter_amd import _lib  # noqa: E402
-from distributed_bitcoin_minter_amd._lib import Context, device_count, device_pci_bus_id, rccl_unique_id  # noqa: E402
-from distributed_bitcoin_minter_amd.dist import lex_min, rank_piece, shares_from_rates  # noqa: E402
+from distributed_bitcoin_minter_amd._lib import (COMBINED_NAMES, Context, device_count,  # noqa: E402
+                                                 device_pci_bus_id, rccl_unique_id)
+from distributed_bitcoin_minter_amd.dist import lex_min, shares_from_rates  # noqa: E402
 
 U64 = (1 << 64) - 1
 PER_GPU = 1 << 32
@@ -199,6 +200,28 @@ class ClockSampler:
         return sum(self.samples) / len(self.samples) / 1e9 if self.samples else None
 
 
+def measure_clock(dev, msg, digits, lo, hi, seconds=0.5, max_nonces=1 << 32):
+    """The driver's gfx clock of GPU `dev` while the dominant kernel runs:
+    hwmon freq1_input sampled every 10 ms over untimed searches of that
+    kernel's digit range (at most 2^32 nonces of it) on a context of its own,
+    so the step's smaller launches (which clock higher) do not bias it.
+    Returns {ghz, lower, upper, searches} or None where sysfs has no clock."""
+    a = max(lo, 10 ** (digits - 1))
+    b = min(hi, 10 ** digits - 1, a + max_nonces - 1)
+    if a > b:
+        return None
+    with Context(devices=[dev]) as c:
+        c.search(msg, a, b)
+        smp = ClockSampler(dev, period=0.01)
+        smp.start()
+        t, k = time.perf_counter(), 0
+        while k < 3 or time.perf_counter() - t < seconds:
+            c.search(msg, a, b)
+            k += 1
+        ghz = smp.stop()
+    return {"ghz": ghz, "lower": a, "upper": b, "searches": k} if ghz else None
+
+
 def hip_runtimes():
     """HIP runtime libraries mapped into this process."""
     try:
@@ -320,21 +343,15 @@ class Group:
             self.rdzv.close()
 
 
-# The range partitioner's shares for the torchrun ranks (None: near-equal
-# pieces).  Ranks of the library's RCCL group ("library": True) get them
-# through ctx.set_split; the rendezvous-gather paths cut their pieces with
-# dist.rank_piece, the mirror of the library's partitioner.
-SPLIT = {"shares": None, "library": False}
-
-
 def calibrate_split(args, ctx, grp):
     """After the warmup (ranks: at least 2 steps, so the one timed is warm):
     each GPU's rate in the last warmup step (its own
     nonces over its launches' span, HIP events, so the wait for the other
     ranks does not count) -> integer shares, the same on every rank -> the
-    timed steps cut the range in proportion (bm_ctx_set_split).
-    A one-process multi-device context balances itself (bm_ctx_set_balance).
-    Returns what the bench line reports."""
+    timed steps cut the range in proportion (bm_ctx_set_split on every rank's
+    context, joined to the RCCL group or not).  A one-process
+    multi-device context balances itself (bm_ctx_set_balance).  Returns what
+    the bench line reports."""
     if args.no_balance or args.warmup < 1:
         return {"mode": "near-equal"}
     if grp.world > 1 and args.warmup < 2:
@@ -352,74 +369,93 @@ def calibrate_split(args, ctx, grp):
     if min(rates) <= 0:
         return {"mode": "near-equal", "note": "a rank's piece was too small to time"}
     shares = shares_from_rates(rates)
-    if SPLIT["library"]:
-        ctx.set_split(shares)
-    SPLIT["shares"] = shares
+    ctx.set_split(shares)
     return {"mode": "measured rank rates, last warmup step", "shares": shares,
             "rates_nonces_per_ms": [round(r, 1) for r in rates]}
 
 
+JOIN_TIMEOUT_MS = 120_000  # a group that has not formed by then falls back to the rendezvous gather
+PEER_TIMEOUT_MS = 120_000  # a joined rank waits at most this long for the others' partials
+
+
+def rank_device(args, local):
+    """The GPU a torchrun rank drives.  A launcher may give every rank a
+    one-device visibility mask (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES per
+    rank): then the one visible device is the rank's, whatever its
+    LOCAL_RANK.  With several devices visible, LOCAL_RANK picks one."""
+    if args.rehearse_one_gpu:
+        return 0
+    n = device_count()
+    if n <= 1:
+        return 0  # one device visible (a per-rank mask, or a one-GPU box); none: the context fails loudly
+    if local < n:
+        return local
+    log(f"error: LOCAL_RANK {local} but only {n} HIP devices visible "
+        "(--rehearse-one-gpu runs every rank on GPU 0)")
+    sys.exit(2)
+
+
 def open_contexts(args, world, rank, local):
-    """(ctx, group, search, parallelism) for the launch mode (module docstring)."""
+    """(ctx, group, search, parallelism, device) for the launch mode (module
+    docstring)."""
     if world > 1:
         from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
-        if not args.rehearse_one_gpu and local >= device_count():
-            log(f"error: LOCAL_RANK {local} but only {device_count()} HIP device(s) visible "
-                "(--rehearse-one-gpu runs every rank on GPU 0)")
-            sys.exit(2)
+        dev = rank_device(args, local)
         grp = Group(Rendezvous())
-        if args.rehearse_one_gpu or args.combine == "gather":
-            # every rank scans its piece on its own context; the 16-byte
-            # partials are gathered over the rendezvous
-            dev = 0 if args.rehearse_one_gpu else local
-            ctx = Context(devices=[dev])
-
-            def search(msg, lo, hi):
-                piece = rank_piece(lo, hi, grp.rank, grp.world, SPLIT["shares"])
-                part = ctx.search(msg, *piece) if piece else (U64, U64)
-                return lex_min(tuple(p) for p in grp.gather(list(part)))
-            how = f"{world} processes (one per GPU), rendezvous gather of 16 B partials"
-            if args.rehearse_one_gpu:
-                how += " [rehearsal: every rank on GPU 0]"
-            return ctx, grp, search, how
-        uid = grp.rdzv.broadcast_bytes(rccl_unique_id() if grp.rank == 0 else None)
+        # step 1: every rank opens its rank context (its piece of every search,
+        # no communicator yet) and the ranks compare notes, so no rank joins
+        # RCCL while a peer has already failed
         ctx, err = None, None
         try:
-            ctx = Context(devices=[local], rank=grp.rank, world=grp.world, unique_id=uid)
+            ctx = Context(devices=[dev], rank=grp.rank, world=grp.world)
         except _lib.BtcMinerError as e:
-            err = str(e)
+            err = f"rank {grp.rank}: {e}"
         errs = [x for x in grp.gather(err) if x]
-        if not errs:
-            SPLIT["library"] = True
-            return ctx, grp, ctx.search, f"{world} processes (one per GPU), RCCL allgather of 16 B partials in-library"
-        # every rank saw the failure: fall back to gathering the partials over
-        # the rendezvous (the measurement is the same search; the combine is 16 B)
-        log(f"rank {grp.rank}: RCCL group failed ({errs[0]}); gathering the partials over the rendezvous instead")
-        if ctx is not None:
-            ctx.close()
-        ctx = Context(devices=[local])
+        if errs:
+            log(f"error: {errs[0]}")
+            if ctx is not None:
+                ctx.close()
+            grp.close()
+            sys.exit(1)
+        why = "rehearsal: every rank on GPU 0" if args.rehearse_one_gpu else "--combine gather"
+        if args.combine == "rccl" and not args.rehearse_one_gpu:
+            # step 2: rank 0's unique id over the rendezvous; every rank joins
+            # (non-blocking init, bounded); all or none keep the group
+            uid = grp.rdzv.broadcast_bytes(rccl_unique_id() if grp.rank == 0 else None)
+            jerr = None
+            try:
+                ctx.join(uid, timeout_ms=JOIN_TIMEOUT_MS)
+            except _lib.BtcMinerError as e:
+                jerr = f"rank {grp.rank}: {e}"
+            jerrs = [x for x in grp.gather(jerr) if x]
+            if not jerrs:
+                ctx.set_peer_timeout(PEER_TIMEOUT_MS)
+                return ctx, grp, ctx.search, f"{world} processes (one per GPU), RCCL allgather of 32 B slots in-library", dev
+            if ctx.joined():
+                ctx.leave()
+            why = f"RCCL group failed: {jerrs[0]}"
+            log(f"rank {grp.rank}: {why}; gathering the partials over the rendezvous instead")
 
+        # each rank's context returns its own piece's partial; the 16-byte
+        # partials meet over the rendezvous (the same search; the combine is 16 B)
         def search(msg, lo, hi):
-            piece = rank_piece(lo, hi, grp.rank, grp.world, SPLIT["shares"])
-            part = ctx.search(msg, *piece) if piece else (U64, U64)
-            return lex_min(tuple(p) for p in grp.gather(list(part)))
-        return ctx, grp, search, (f"{world} processes (one per GPU), rendezvous gather of 16 B partials "
-                                  f"(RCCL failed: {errs[0]})")
+            return lex_min(tuple(p) for p in grp.gather(list(ctx.search(msg, lo, hi))))
+        return ctx, grp, search, f"{world} processes (one per GPU), rendezvous gather of 16 B partials ({why})", dev
     grp = Group()
     n = args.gpus
     if n > 1:
         if args.rehearse_one_gpu:
             ctx = Context(devices=[0] * n)  # same device n times: host combine
-            return ctx, grp, ctx.search, f"one process, {n}-way split on GPU 0 [rehearsal], host combine"
+            return ctx, grp, ctx.search, f"one process, {n}-way split on GPU 0 [rehearsal]", 0
         have = device_count()
         if have < n:
             log(f"error: --gpus {n} but only {have} HIP device(s) visible "
                 "(use torchrun for one process per GPU, or --rehearse-one-gpu to check the split on one GPU)")
             sys.exit(2)
         ctx = Context(num_gpus=n)
-        return ctx, grp, ctx.search, f"one process, {n} devices, RCCL ncclAllGather of 16 B partials in-library"
+        return ctx, grp, ctx.search, f"one process, {n} devices", 0
     ctx = Context(devices=[local])
-    return ctx, grp, ctx.search, "1 device"
+    return ctx, grp, ctx.search, "1 device", local
 
 
 def main():
@@ -450,7 +486,7 @@ def main():
         sys.exit(2)
     _lib.load()  # before anything else can map a second HIP runtime
 
-    ctx, grp, search, how = open_contexts(args, world, rank, local)
+    ctx, grp, search, how, dev = open_contexts(args, world, rank, local)
     ctx.set_timing(True)
     if world == 1 and ctx.num_devices() > 1 and not args.no_balance:
         ctx.set_balance(True)
@@ -465,13 +501,16 @@ def main():
         # this device's algorithmic ops over the call's GPU span (first
         # launch start to last launch end): launches overlap on two streams
         ops = sum(L.nonces * (L.nbv + L.pad_block) for L in launches) * OPS_PER_COMPRESSION
-        return res, (dom, ops, st.span_ms)
+        per = {"nonces": st.nonces, "span_ms": st.span_ms, "combine": COMBINED_NAMES.get(st.combine_used, "?"),
+               "rccl_status": st.rccl_status,
+               "devices": [(st.dev_nonces[i], st.dev_span_ms[i]) for i in range(st.devices)]}
+        return res, (dom, ops, st.span_ms, per)
 
     for _ in range(args.warmup):
         step()
     split = calibrate_split(args, ctx, grp)
-    sampler = ClockSampler(0 if args.rehearse_one_gpu else (local if world > 1 else 0),
-                           period=0.05 if (args.clock_sample if args.clock_sample is not None else n > 1) else None)
+    sampler = ClockSampler(dev, period=0.05 if (args.clock_sample if args.clock_sample is not None else n > 1)
+                           else None)
     grp.barrier()
     sampler.start()
     t0 = time.perf_counter()
@@ -485,12 +524,40 @@ def main():
     grp.barrier()
     dt = grp.max(dt)
     clocks = grp.gather(sysfs_clock) if world > 1 else [sysfs_clock]
+    # the clock under the dominant kernel on THIS box, for the issue bound
+    # (untimed, after the timed region; every rank on its own GPU)
+    dom0 = doms[-1][0]
+    box_clock = measure_clock(dev, msg, dom0.digits, lo, hi) if dom0 is not None else None
+    grp.barrier()
 
     total = hi - lo + 1
     value = total * args.steps / dt / 1e9
     want = golden(msg, lo, hi)
     dom = doms[-1][0]
-    calls = [(o, sp) for _, o, sp in doms if sp > 0]
+    calls = [(o, sp) for _, o, sp, _p in doms if sp > 0]
+    pers = [d[3] for d in doms]
+    combine = pers[-1]["combine"]
+    mean = lambda xs: sum(xs) / len(xs) if xs else 0.0
+    if world > 1:
+        # each rank's share of the timed steps: its nonces, its GPU span, its
+        # rate, how the partials met, and its GPU clock (driver hwmon)
+        mine = {"rank": grp.rank, "device": dev, "nonces": pers[-1]["nonces"],
+                "span_ms": round(mean([p["span_ms"] for p in pers]), 3), "combine": combine,
+                "clock_ghz_sysfs": None if sysfs_clock is None else round(sysfs_clock, 3)}
+        mine["GHs"] = round(mine["nonces"] / mine["span_ms"] / 1e6, 3) if mine["span_ms"] > 0 else None
+        if pers[-1]["rccl_status"]:
+            mine["rccl_status"] = pers[-1]["rccl_status"]
+        slots = grp.gather(mine)
+        how += f"; combine {combine}"
+    else:
+        slots = []
+        for i, (nn, _sp) in enumerate(pers[-1]["devices"]):
+            sp = mean([p["devices"][i][1] for p in pers])
+            slots.append({"device": i, "nonces": nn, "span_ms": round(sp, 3),
+                          "GHs": round(nn / sp / 1e6, 3) if sp > 0 else None})
+        if n > 1:
+            how += f"; combine {combine}" + (f" (RCCL failed, status {pers[-1]['rccl_status']}: host copies)"
+                                             if pers[-1]["rccl_status"] else "")
     out = {
         "metric": METRIC,
         "value": round(value, 4),
@@ -505,7 +572,8 @@ def main():
         "dtype": "u32",
         "data": "synthetic",
         "config": {"workload": desc, "name": args.config, "msg": msg.decode(), "lower": lo, "upper": hi,
-                   "global_nonces": total, "parallelism": how, "split": split},
+                   "global_nonces": total, "parallelism": how, "split": split,
+                   ("ranks" if world > 1 else "devices"): slots},
         "result": list(res),
         "golden": want,
         "result_ok": None if want is None else list(res) == want,
@@ -546,28 +614,33 @@ def main():
             roof["valu_dual_issued_frac_pmc"] = round(cnt["SQ_ACTIVE_INST_VALU2"] / cnt["SQ_INSTS_VALU"], 4)
         if clock:
             roof["clock_ghz_pmc"] = round(clock, 3)
-        # the live clock under the dominant launch (s_memtime / s_memrealtime
-        # stamped by workgroup 0, averaged over the timed steps); the PMC clock
-        # of the committed profile otherwise (another run, maybe another box)
+        # the clock under the dominant kernel on this box: live stamps
+        # (s_memtime / s_memrealtime, BM_CLOCK_PROBE builds), else the
+        # driver's gfx clock sampled while that kernel's range ran alone
+        # (measure_clock).  The committed PMC clock (clock_ghz_pmc) is another
+        # run, maybe another box: it is never used for the fraction.
         live = [d[0].clock_ghz for d in doms if d[0] is not None and d[0].clock_ghz > 0]
         live_clock = sum(live) / len(live) if live else None
         if live_clock:
             roof["clock_ghz_live"] = round(live_clock, 3)
         if sysfs_clock:
-            # the driver's gfx clock over the timed region: on one box it read
-            # 2.235-2.241 GHz where PMC put the dominant launch at 2.20-2.22
-            # (profiles/r02/s2_clock_sources.log), so it is reported, not used
+            # the driver's gfx clock over the whole timed steps (every launch)
             roof["clock_ghz_sysfs"] = round(sysfs_clock, 3)
-        ib_clock = live_clock or clock
-        if ib_clock:
-            ib = issue_bound(dom.p, dom.nbv, ib_clock)
-            if ib:
-                ib["clock_src"] = "live (s_memtime / s_memrealtime)" if live_clock else pmc_src
+        box = box_clock or {}
+        if box.get("ghz"):
+            roof["clock_ghz_box"] = round(box["ghz"], 3)
+        ib_clock = live_clock or box.get("ghz")
+        ib = issue_bound(dom.p, dom.nbv, ib_clock or clock or 0.0) if (ib_clock or clock) else None
+        if ib:
+            if ib_clock:
+                ib["clock_src"] = ("live (s_memtime / s_memrealtime)" if live_clock else
+                                   f"this box: hwmon freq1_input every 10 ms over {box['searches']} untimed "
+                                   f"searches of the dominant kernel's range [{box['lower']}, {box['upper']}]")
                 ib["frac"] = round(dom.nonces / (dom_ms * 1e-3) / 1e9 / ib["GHs_per_gpu"], 4)
-                if not live_clock:
-                    ib["note"] = ("clock from the committed PMC profile (another run; boxes run this kernel at "
-                                  "2.04-2.23 GHz), so frac can exceed 1 on a faster box")
-                roof["issue_bound"] = ib
+            else:
+                ib["clock_src"] = pmc_src
+                ib["note"] = "no clock measured on this box: the bound at the committed PMC clock, no frac"
+            roof["issue_bound"] = ib
         if calls:
             # the whole call on this device: every launch's algorithmic ops over
             # the span of its launches (two streams overlap launches, which

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# BTCMINER_LIB overrides the library path (used to A/B kernel build variants)
+# BTCMINER_LIB overrides the library path (used to A/B kernel build variants;
+# they must be built from the same ABI version)
 LIB_PATH = os.environ.get("BTCMINER_LIB") or os.path.join(_HERE, "libbtcminer.so")
 
 BM_OK = 0
@@ -18,10 +19,16 @@ BM_EHIP = -3
 BM_ERCCL = -4
 BM_ENOMEM = -5
 BM_EINTERNAL = -6
+BM_EPEER = -7
+BM_ETIMEDOUT = -8
 BM_MAX_LAUNCH_STATS = 64
+BM_MAX_STAT_DEVICES = 16
 BM_RCCL_ID_BYTES = 128
-BM_ABI_VERSION = 4
+BM_ABI_VERSION = 5
 BM_COMBINE_AUTO, BM_COMBINE_RCCL, BM_COMBINE_HOST = 0, 1, 2
+# bm_stats_t.combine_used
+BM_COMBINED_NONE, BM_COMBINED_RCCL, BM_COMBINED_HOST, BM_COMBINED_LOCAL = 0, 1, 2, 3
+COMBINED_NAMES = {0: "none", 1: "rccl", 2: "host", 3: "local"}
 U64_MAX = (1 << 64) - 1
 
 c_u64 = ctypes.c_uint64
@@ -42,6 +49,8 @@ class LaunchStat(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("launches", c_u32), ("recorded", c_u32), ("wall_ms", ctypes.c_double),
                 ("kernel_ms", ctypes.c_double), ("span_ms", ctypes.c_double), ("nonces", c_u64),
+                ("combine_used", c_i32), ("rccl_status", c_i32), ("devices", c_u32), ("reserved", c_u32),
+                ("dev_nonces", c_u64 * BM_MAX_STAT_DEVICES), ("dev_span_ms", ctypes.c_double * BM_MAX_STAT_DEVICES),
                 ("launch", LaunchStat * BM_MAX_LAUNCH_STATS)]
 
 
@@ -86,6 +95,12 @@ def load():
         "bm_ctx_num_devices": ([vp, P(ctypes.c_int)], ctypes.c_int),
         "bm_rccl_unique_id": ([ctypes.c_char_p], ctypes.c_int),
         "bm_ctx_create_rank": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, P(vp)], ctypes.c_int),
+        "bm_ctx_create_rank_local": ([ctypes.c_int, ctypes.c_int, ctypes.c_int, P(vp)], ctypes.c_int),
+        "bm_ctx_join_rank": ([vp, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
+        "bm_ctx_leave_rank": ([vp], ctypes.c_int),
+        "bm_ctx_rank_joined": ([vp, P(ctypes.c_int)], ctypes.c_int),
+        "bm_ctx_set_peer_timeout": ([vp, ctypes.c_int], ctypes.c_int),
+        "bm_ctx_set_test_rccl_fault": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_ctx_rank": ([vp, P(ctypes.c_int), P(ctypes.c_int)], ctypes.c_int),
         "bm_reduce_gpu": ([vp, P(Result), ctypes.c_size_t, P(Result)], ctypes.c_int),
         "bm_ctx_set_test_fault": ([vp, ctypes.c_int], ctypes.c_int),
@@ -111,9 +126,9 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
-    # an explicit BTCMINER_LIB (A/B of older builds, tools/ab_bench.py) may
-    # predate the current stats layout; the in-tree library must match
-    if lib.bm_abi_version() != BM_ABI_VERSION and not os.environ.get("BTCMINER_LIB"):
+    # the stats structs above are this ABI's layout: any other build (an
+    # older BTCMINER_LIB variant included) would be misread, so it is refused
+    if lib.bm_abi_version() != BM_ABI_VERSION:
         raise OSError(f"{LIB_PATH}: ABI version {lib.bm_abi_version()}, expected {BM_ABI_VERSION}; rebuild it")
     _lib = lib
     return lib
@@ -179,18 +194,26 @@ class Context:
     """Owns a bm_ctx over one or more GPUs.  Not thread-safe (like the C ctx).
 
     Context(devices=[...]) / Context(num_gpus=N): one process, N devices.
-    Context(devices=[d], rank=r, world=w, unique_id=uid): rank r of an RCCL
-    process group (one process per GPU); blocks until all w ranks join."""
+    Context(devices=[d], rank=r, world=w): rank r of w (one process per GPU)
+    outside a group: search() scans rank r's piece and returns its partial;
+    join(uid) then makes it a member of the RCCL group.
+    Context(devices=[d], rank=r, world=w, unique_id=uid): both steps at once
+    (blocks until all w ranks join)."""
 
     def __init__(self, devices=None, num_gpus=0, rank=None, world=None, unique_id=None):
         lib = load()
         h = ctypes.c_void_p()
         if world is not None:
-            if devices is None or len(devices) != 1 or rank is None or unique_id is None:
-                raise ValueError("a rank context takes devices=[device], rank, world and unique_id")
-            if len(unique_id) != BM_RCCL_ID_BYTES:
-                raise ValueError(f"unique_id must be {BM_RCCL_ID_BYTES} bytes")
-            check(lib.bm_ctx_create_rank(devices[0], rank, world, unique_id, ctypes.byref(h)), "bm_ctx_create_rank")
+            if devices is None or len(devices) != 1 or rank is None:
+                raise ValueError("a rank context takes devices=[device], rank and world")
+            if unique_id is None:
+                check(lib.bm_ctx_create_rank_local(devices[0], rank, world, ctypes.byref(h)),
+                      "bm_ctx_create_rank_local")
+            else:
+                if len(unique_id) != BM_RCCL_ID_BYTES:
+                    raise ValueError(f"unique_id must be {BM_RCCL_ID_BYTES} bytes")
+                check(lib.bm_ctx_create_rank(devices[0], rank, world, unique_id, ctypes.byref(h)),
+                      "bm_ctx_create_rank")
         elif devices is not None:
             ids = (ctypes.c_int * len(devices))(*devices)
             check(lib.bm_ctx_create_devices(ids, len(devices), ctypes.byref(h)), "bm_ctx_create_devices")
@@ -232,6 +255,26 @@ class Context:
         r, w = ctypes.c_int(0), ctypes.c_int(0)
         check(self._lib.bm_ctx_rank(self.handle, ctypes.byref(r), ctypes.byref(w)), "bm_ctx_rank")
         return r.value, w.value
+
+    def join(self, unique_id: bytes, timeout_ms: int = 0):
+        """Join the RCCL group (bm_ctx_join_rank): every rank, same id."""
+        if len(unique_id) != BM_RCCL_ID_BYTES:
+            raise ValueError(f"unique_id must be {BM_RCCL_ID_BYTES} bytes")
+        check(self._lib.bm_ctx_join_rank(self.handle, unique_id, timeout_ms), "bm_ctx_join_rank")
+
+    def leave(self):
+        check(self._lib.bm_ctx_leave_rank(self.handle), "bm_ctx_leave_rank")
+
+    def joined(self) -> bool:
+        j = ctypes.c_int(0)
+        check(self._lib.bm_ctx_rank_joined(self.handle, ctypes.byref(j)), "bm_ctx_rank_joined")
+        return bool(j.value)
+
+    def set_peer_timeout(self, timeout_ms: int):
+        check(self._lib.bm_ctx_set_peer_timeout(self.handle, timeout_ms), "bm_ctx_set_peer_timeout")
+
+    def set_test_rccl_fault(self, where: int):
+        check(self._lib.bm_ctx_set_test_rccl_fault(self.handle, where), "bm_ctx_set_test_rccl_fault")
 
     def reduce(self, pairs):
         """Lexicographic min of (hash, nonce) pairs by the GPU reductions

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "bm_aux_kernels.hpp"
@@ -43,6 +44,17 @@ constexpr size_t kCtrStride = 32;  // u64 words per launch: counter [0], clock s
 constexpr uint64_t kBalanceMinNonces = 1ull << 30;
 constexpr double kShareScale = 65536.0;
 
+// What each device / rank contributes to the combine: its partial and a
+// status word (a rank that failed the call before the combine still takes
+// part in the allgather, with its status here).  32 bytes = 4 u64.
+struct Slot {
+    Partial p;
+    uint64_t status;
+    uint64_t pad;
+};
+static_assert(sizeof(Slot) == 32, "slot layout");
+constexpr size_t kSlotWords = sizeof(Slot) / sizeof(uint64_t);
+
 struct DeviceCtx {
     int id = -1;
     int cus = 0;
@@ -53,9 +65,10 @@ struct DeviceCtx {
                                           // counter, [16..19] clock stamps (bm_kernels.hpp)
     unsigned long long* h_ctr = nullptr;  // pinned copy of the strips (timing on)
     size_t ctr_cap = 0;
-    Partial* d_result = nullptr;  // 1 partial
-    Partial* d_gather = nullptr;  // nslots partials (allgather target)
-    Partial* h_result = nullptr;  // pinned, nslots partials
+    Slot* d_slot = nullptr;    // this device's slot (reduce_partials writes its partial)
+    Slot* d_gather = nullptr;  // nslots slots (allgather target)
+    Slot* h_slots = nullptr;   // pinned: nslots slots, + 1 staging slot (a failed rank's status)
+    int nslots = 1;
     Partial* d_test = nullptr;    // bm_reduce_gpu's staging buffer
     size_t test_cap = 0;
     uint64_t* d_hash_io = nullptr;
@@ -63,9 +76,10 @@ struct DeviceCtx {
     hipEvent_t ev[2 * kEventPairs] = {};
     hipStream_t aux[kMaxStreams - 1] = {};  // extra launch streams (ctx->streams > 1)
     hipEvent_t fork = nullptr, join[kMaxStreams - 1] = {};
-    hipEvent_t bal[2] = {};     // balance: the device's first op and its reduction (timing events)
+    hipEvent_t bal[2] = {};     // the device's first op and the end of its reduction (balance, timing)
+    hipEvent_t own_done = nullptr;  // rank contexts: this rank's reduction done (before the allgather)
     uint64_t piece_nonces = 0;  // nonces of the device's piece in the last call
-    ncclComm_t comm = nullptr;  // multi-device ctx: ncclCommInitAll; rank ctx: the process group's
+    ncclComm_t comm = nullptr;  // multi-device ctx: ncclCommInitAll; joined rank ctx: the process group's
     std::vector<std::pair<const void*, int>> occ;  // kernel -> blocks per CU
     double wall_clock_hz = 100e6;                  // s_memrealtime rate
 };
@@ -110,8 +124,14 @@ struct bm_ctx {
     uint64_t tail_nonces = 1ull << 24;  // split off the biggest launch's last nonces (BTCMINER_TAIL; 0: off; profiles/r01/ab_tail.log)
     int streams = 2;      // launch streams per device (1..kMaxStreams; BTCMINER_STREAMS; profiles/r01/ab_streams.log)
     bool nccl_ready = false;
-    int rank = 0, world = 1;  // bm_ctx_create_rank: this process's place in an RCCL process group
+    int rccl_status = 0;      // multi-device ctx: the RCCL failure it fell back from (then: host copies)
+    int rank = 0, world = 1;  // rank contexts: this process's place in the group
+    bool rank_ctx = false;    // made by bm_ctx_create_rank_local (one device, one slot of `world`)
+    bool joined = false;      // rank ctx: member of an RCCL group (devs[0].comm)
+    int group_status = 0;     // joined rank ctx whose communicator failed (BM_ERCCL / BM_ETIMEDOUT)
+    int peer_timeout_ms = 0;  // joined rank ctx: wait at most this long for the group (0: no limit)
     int fault_after = -1;     // test hook: fail after enqueueing this many launches (-1: off)
+    int test_rccl_fault = 0;  // test hook: 1 communicator set-up fails, 2 every allgather fails
     uint64_t lane_chunk = bm::kNoncesPerLaneChunk;  // nonces per lane per dequeue, at most (BTCMINER_CHUNK)
     std::vector<uint32_t> shares;  // the partitioner's shares per slot (empty: near-equal pieces)
     bool balance = false;          // multi-device: shares follow each device's measured rate
@@ -241,14 +261,16 @@ int init_device(DeviceCtx& d, int id, int nslots) {
     if (hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, id) == hipSuccess && wall_khz > 0)
         d.wall_clock_hz = 1e3 * wall_khz;
     BM_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    BM_HIP(hipMalloc(&d.d_result, sizeof(Partial)));
-    BM_HIP(hipMalloc(&d.d_gather, sizeof(Partial) * (size_t)nslots));
-    BM_HIP(hipHostMalloc(&d.h_result, sizeof(Partial) * (size_t)nslots, hipHostMallocDefault));
+    d.nslots = nslots;
+    BM_HIP(hipMalloc(&d.d_slot, sizeof(Slot)));
+    BM_HIP(hipMalloc(&d.d_gather, sizeof(Slot) * (size_t)nslots));
+    BM_HIP(hipHostMalloc(&d.h_slots, sizeof(Slot) * (size_t)(nslots + 1), hipHostMallocDefault));
     for (auto& e : d.ev) BM_HIP(hipEventCreate(&e));
     for (auto& s : d.aux) BM_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     BM_HIP(hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
     for (auto& e : d.join) BM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : d.bal) BM_HIP(hipEventCreate(&e));
+    BM_HIP(hipEventCreateWithFlags(&d.own_done, hipEventDisableTiming));
     int rc = ensure_counters(d, 256);
     if (rc != BM_OK) return rc;
     return ensure_partials(d, 4096);
@@ -261,16 +283,18 @@ void destroy_device(DeviceCtx& d) {
     for (auto& s : d.aux)
         if (s) (void)hipStreamSynchronize(s);
     if (d.comm) (void)ncclCommDestroy(d.comm);
+    d.comm = nullptr;
     for (auto& e : d.ev)
         if (e) (void)hipEventDestroy(e);
     if (d.d_part) (void)hipFree(d.d_part);
     if (d.d_ctr) (void)hipFree(d.d_ctr);
     if (d.h_ctr) (void)hipHostFree(d.h_ctr);
-    if (d.d_result) (void)hipFree(d.d_result);
+    if (d.d_slot) (void)hipFree(d.d_slot);
     if (d.d_gather) (void)hipFree(d.d_gather);
     if (d.d_hash_io) (void)hipFree(d.d_hash_io);
     if (d.d_test) (void)hipFree(d.d_test);
-    if (d.h_result) (void)hipHostFree(d.h_result);
+    if (d.h_slots) (void)hipHostFree(d.h_slots);
+    if (d.own_done) (void)hipEventDestroy(d.own_done);
     for (auto& e : d.join)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : d.bal)
@@ -293,6 +317,7 @@ int ensure_nccl(bm_ctx* ctx) {
     // an RCCL communicator holds one rank per GPU: a device listed twice
     // (a one-GPU rehearsal of the N-device split) combines on the host
     if (!distinct_devices(ctx)) return BM_EINVAL;
+    if (ctx->test_rccl_fault == 1) return BM_ERCCL;  // test hook
     const int n = (int)ctx->devs.size();
     std::vector<ncclComm_t> comms(n);
     std::vector<int> ids(n);
@@ -301,6 +326,29 @@ int ensure_nccl(bm_ctx* ctx) {
     for (int i = 0; i < n; ++i) ctx->devs[i].comm = comms[i];
     ctx->nccl_ready = true;
     return BM_OK;
+}
+
+// Drops every communicator of the context after a failure (ncclCommAbort:
+// also ends any collective of it still queued on a stream).
+void abort_nccl(bm_ctx* ctx) {
+    for (auto& d : ctx->devs) {
+        if (!d.comm) continue;
+        (void)hipSetDevice(d.id);
+        (void)ncclCommAbort(d.comm);
+        d.comm = nullptr;
+    }
+    ctx->nccl_ready = false;
+}
+
+// A non-blocking communicator's last operation: wait until it leaves
+// ncclInProgress (or the deadline passes: BM_ETIMEDOUT).
+int comm_settle(ncclComm_t comm, ncclResult_t r, std::chrono::steady_clock::time_point deadline, bool limited) {
+    while (r == ncclInProgress) {
+        if (limited && std::chrono::steady_clock::now() > deadline) return BM_ETIMEDOUT;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) return BM_ERCCL;
+    }
+    return r == ncclSuccess ? BM_OK : BM_ERCCL;
 }
 
 // Waits for everything a call may have queued on any stream of the context.
@@ -317,11 +365,12 @@ void drain(bm_ctx* ctx) {
     (void)hipGetLastError();
 }
 
-// Stages 2-3 of a search: enqueue every launch and the second-pass
-// reduction, combine the partials, wait.  On failure the caller drains.
-int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches, std::vector<uint32_t>& first,
-                        Partial* best_out) {
+// Stage 2 of a search: enqueue every launch and the second-pass reduction
+// of each device (its partial lands in d_slot).  On failure the caller drains.
+int enqueue(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches, std::vector<uint32_t>& first) {
     const int ndev = (int)ctx->devs.size();
+    const bool mark = ctx->balance || ctx->timing;  // per-device span events
+    if (ctx->fault_after == 0) return BM_EINTERNAL;  // test hook (also for a rank with nothing to scan)
     int enqueued = 0;
     for (int di = 0; di < ndev; ++di) {
         DeviceCtx& d = ctx->devs[di];
@@ -330,7 +379,7 @@ int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches,
         if (!launches[di].empty())
             BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches[di].size() * kCtrStride * sizeof(unsigned long long),
                                   d.stream));
-        if (ctx->balance) BM_HIP(hipEventRecord(d.bal[0], d.stream));
+        if (mark) BM_HIP(hipEventRecord(d.bal[0], d.stream));
         // stream of each launch: biggest first, round-robin over the streams
         const int ns = std::max(1, std::min<int>(ctx->streams, (int)launches[di].size()));
         std::vector<uint32_t> order(launches[di].size());
@@ -362,82 +411,174 @@ int enqueue_and_combine(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches,
             BM_HIP(hipStreamWaitEvent(d.stream, d.join[k], 0));
         }
         // nparts = 0 (a device or rank with nothing to scan) writes (2^64-1, 2^64-1)
-        reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, d.d_result);
+        reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, &d.d_slot->p);
         BM_HIP(hipGetLastError());
-        if (ctx->balance) BM_HIP(hipEventRecord(d.bal[1], d.stream));
+        if (mark) BM_HIP(hipEventRecord(d.bal[1], d.stream));
         if (BM_CLOCK_PROBE && ctx->timing && !launches[di].empty())  // clock stamps, for the launch stats
             BM_HIP(hipMemcpyAsync(d.h_ctr, d.d_ctr, launches[di].size() * kCtrStride * sizeof(unsigned long long),
                                   hipMemcpyDeviceToHost, d.stream));
     }
+    return BM_OK;
+}
 
-    // 3. combine: one RCCL allgather of the 16-byte partials, or plain copies
+Partial lex_min_slots(const Slot* s, int n) {
+    Partial best{UINT64_MAX, UINT64_MAX};
+    for (int i = 0; i < n; ++i) {
+        const Partial& p = s[i].p;
+        if (p.hash < best.hash || (p.hash == best.hash && p.nonce < best.nonce)) best = p;
+    }
+    return best;
+}
+
+// Stage 3 of a search, one process: combine the devices' partials with one
+// RCCL allgather, or by host copies (BM_COMBINE_HOST, a device listed twice,
+// or RCCL failing at run time: the context then aborts its communicators and
+// stays on host copies, reported in the stats).  A rank context outside a
+// group copies its own partial.
+int combine_local(bm_ctx* ctx, Partial* best_out) {
+    bm_stats_t& st = ctx->stats;
+    const int ndev = (int)ctx->devs.size();
     int nslots = ndev;
-    if (ctx->world > 1) {
-        // one device per rank: gather every rank's partial over the process group
-        DeviceCtx& d = ctx->devs[0];
-        if (ncclAllGather(d.d_result, d.d_gather, 2, ncclUint64, d.comm, d.stream) != ncclSuccess) return BM_ERCCL;
-        BM_HIP(hipMemcpyAsync(d.h_result, d.d_gather, sizeof(Partial) * ctx->world, hipMemcpyDeviceToHost, d.stream));
-        nslots = ctx->world;
-    } else {
-        const bool use_rccl = ctx->combine == BM_COMBINE_RCCL ||
-                              (ctx->combine == BM_COMBINE_AUTO && ndev > 1 && distinct_devices(ctx));
-        if (use_rccl) {
+    bool via_rccl = false;
+    if (!ctx->rank_ctx) {
+        const bool distinct = distinct_devices(ctx);
+        if (ctx->combine == BM_COMBINE_RCCL && !distinct) return BM_EINVAL;
+        const bool want = ctx->combine == BM_COMBINE_RCCL || (ctx->combine == BM_COMBINE_AUTO && ndev > 1 && distinct);
+        if (want && ctx->rccl_status == 0) {
             int rc = ensure_nccl(ctx);
-            if (rc != BM_OK) return rc;
-            if (ncclGroupStart() != ncclSuccess) return BM_ERCCL;
-            for (int di = 0; di < ndev; ++di) {
-                DeviceCtx& d = ctx->devs[di];
-                if (ncclAllGather(d.d_result, d.d_gather, 2, ncclUint64, d.comm, d.stream) != ncclSuccess) {
-                    (void)ncclGroupEnd();
-                    return BM_ERCCL;
+            if (rc == BM_OK) {
+                for (int di = 0; di < ndev && rc == BM_OK; ++di) {
+                    DeviceCtx& d = ctx->devs[di];
+                    if (hipSetDevice(d.id) != hipSuccess ||
+                        hipMemsetAsync(&d.d_slot->status, 0, 2 * sizeof(uint64_t), d.stream) != hipSuccess)
+                        return BM_EHIP;
+                }
+                if (ctx->test_rccl_fault == 2) {
+                    rc = BM_ERCCL;  // test hook: as if the grouped allgather failed
+                } else if (ncclGroupStart() != ncclSuccess) {
+                    rc = BM_ERCCL;
+                } else {
+                    for (int di = 0; di < ndev && rc == BM_OK; ++di) {
+                        DeviceCtx& d = ctx->devs[di];
+                        if (ncclAllGather(d.d_slot, d.d_gather, kSlotWords, ncclUint64, d.comm, d.stream) !=
+                            ncclSuccess)
+                            rc = BM_ERCCL;
+                    }
+                    if (ncclGroupEnd() != ncclSuccess) rc = BM_ERCCL;
                 }
             }
-            if (ncclGroupEnd() != ncclSuccess) return BM_ERCCL;
-            DeviceCtx& d0 = ctx->devs[0];
-            BM_HIP(hipSetDevice(d0.id));
-            BM_HIP(hipMemcpyAsync(d0.h_result, d0.d_gather, sizeof(Partial) * ndev, hipMemcpyDeviceToHost,
-                                  d0.stream));
-        } else {
-            for (int di = 0; di < ndev; ++di) {
-                DeviceCtx& d = ctx->devs[di];
-                BM_HIP(hipSetDevice(d.id));
-                BM_HIP(hipMemcpyAsync(ctx->devs[0].h_result + di, d.d_result, sizeof(Partial),
-                                      hipMemcpyDeviceToHost, d.stream));
+            if (rc == BM_OK) {
+                DeviceCtx& d0 = ctx->devs[0];
+                BM_HIP(hipSetDevice(d0.id));
+                BM_HIP(hipMemcpyAsync(d0.h_slots, d0.d_gather, sizeof(Slot) * ndev, hipMemcpyDeviceToHost,
+                                      d0.stream));
+                via_rccl = true;
+            } else if (rc == BM_ERCCL) {
+                ctx->rccl_status = rc;  // fall back to host copies, now and for every later call
+                abort_nccl(ctx);
+            } else {
+                return rc;
             }
+        }
+    } else {
+        nslots = 1;  // a rank outside a group: its own partial
+    }
+    if (!via_rccl) {
+        for (int di = 0; di < ndev; ++di) {
+            DeviceCtx& d = ctx->devs[di];
+            BM_HIP(hipSetDevice(d.id));
+            BM_HIP(hipMemcpyAsync(ctx->devs[0].h_slots + di, d.d_slot, sizeof(Partial), hipMemcpyDeviceToHost,
+                                  d.stream));
         }
     }
     for (int di = 0; di < ndev; ++di) {
         BM_HIP(hipSetDevice(ctx->devs[di].id));
         BM_HIP(hipStreamSynchronize(ctx->devs[di].stream));
     }
-
-    Partial best{UINT64_MAX, UINT64_MAX};
-    for (int i = 0; i < nslots; ++i) {
-        const Partial& p = ctx->devs[0].h_result[i];
-        if (p.hash < best.hash || (p.hash == best.hash && p.nonce < best.nonce)) best = p;
-    }
-    *best_out = best;
+    st.combine_used = ctx->rank_ctx ? BM_COMBINED_LOCAL : via_rccl ? BM_COMBINED_RCCL : BM_COMBINED_HOST;
+    st.rccl_status = ctx->rccl_status;
+    *best_out = lex_min_slots(ctx->devs[0].h_slots, nslots);
     return BM_OK;
 }
 
-int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, bm_result_t* out) {
-    const auto t_start = std::chrono::steady_clock::now();
+// Stage 3 of a search, a rank of a group: one allgather of every rank's
+// slot.  A rank whose call failed before this point (own_rc) still takes
+// part, with its status in the slot, so the group fails the call together
+// instead of waiting for it.  The wait for the group after this rank's own
+// work is bounded by peer_timeout_ms (then the communicator is aborted).
+int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
     bm_stats_t& st = ctx->stats;
-    std::memset(&st, 0, sizeof st);
-    const int ndev = (int)ctx->devs.size();
-    if (lower > upper) {  // miner.go:45-46 with zero iterations
-        out->hash = UINT64_MAX;
-        out->nonce = UINT64_MAX;
-        return BM_OK;
+    DeviceCtx& d = ctx->devs[0];
+    const int world = ctx->world;
+    if (hipSetDevice(d.id) != hipSuccess) return BM_EHIP;
+    if (own_rc == BM_OK) {
+        if (hipMemsetAsync(&d.d_slot->status, 0, 2 * sizeof(uint64_t), d.stream) != hipSuccess) return BM_EHIP;
+    } else {
+        Slot& out = d.h_slots[d.nslots];  // pinned staging slot
+        out = Slot{Partial{UINT64_MAX, UINT64_MAX}, (uint64_t)(int64_t)own_rc, 0};
+        if (hipMemcpyAsync(d.d_slot, &out, sizeof(Slot), hipMemcpyHostToDevice, d.stream) != hipSuccess)
+            return BM_EHIP;
     }
+    if (hipEventRecord(d.own_done, d.stream) != hipSuccess) return BM_EHIP;
+    const bool limited = ctx->peer_timeout_ms > 0;
+    int rc = BM_OK;
+    if (ctx->test_rccl_fault == 2) {
+        rc = BM_ERCCL;  // test hook: as if the allgather failed (world 1 only: no peer is left waiting)
+    } else {
+        if (hipEventSynchronize(d.own_done) != hipSuccess) return BM_EHIP;  // own work: no deadline
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ctx->peer_timeout_ms);
+        rc = comm_settle(d.comm, ncclAllGather(d.d_slot, d.d_gather, kSlotWords, ncclUint64, d.comm, d.stream),
+                         deadline, limited);
+        if (rc == BM_OK && hipMemcpyAsync(d.h_slots, d.d_gather, sizeof(Slot) * world, hipMemcpyDeviceToHost,
+                                          d.stream) != hipSuccess)
+            return BM_EHIP;
+        if (rc == BM_OK && !limited) {
+            if (hipStreamSynchronize(d.stream) != hipSuccess) return BM_EHIP;
+        } else if (rc == BM_OK) {
+            for (auto pause = std::chrono::microseconds(10);;) {
+                const hipError_t q = hipStreamQuery(d.stream);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) return BM_EHIP;
+                if (std::chrono::steady_clock::now() > deadline) {
+                    rc = BM_ETIMEDOUT;
+                    break;
+                }
+                std::this_thread::sleep_for(pause);
+                pause = std::min(pause * 2, std::chrono::microseconds(1000));
+            }
+        }
+    }
+    if (rc != BM_OK) {
+        // the communicator cannot be trusted any more: abort it (this also
+        // ends an allgather still waiting on the stream); later searches
+        // return the same status until bm_ctx_leave_rank
+        (void)ncclCommAbort(d.comm);
+        d.comm = nullptr;
+        ctx->group_status = rc;
+        (void)hipStreamSynchronize(d.stream);
+        (void)hipGetLastError();
+        st.rccl_status = rc;
+        return rc;
+    }
+    st.combine_used = BM_COMBINED_RCCL;
+    for (int r = 0; r < world; ++r)
+        if (d.h_slots[r].status != 0) return own_rc != BM_OK ? own_rc : BM_EPEER;
+    if (own_rc != BM_OK) return own_rc;
+    *best_out = lex_min_slots(d.h_slots, world);
+    return BM_OK;
+}
 
-    // 1. this process's piece (rank contexts: every rank passes the same
-    // range and scans its contiguous share of it), split over the devices;
-    // plan and size every launch
-    // (the partitioner: slot_pieces over ctx->shares; an empty piece has lo > hi)
+// Stage 1 of a search: this process's piece (rank contexts: every rank
+// passes the same range and scans its contiguous share of it), split over
+// the devices (the partitioner: slot_pieces over ctx->shares; an empty piece
+// has lo > hi); plan and size every launch.
+int plan_launches(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper,
+                  std::vector<std::vector<Launch>>& launches) {
+    bm_stats_t& st = ctx->stats;
+    const int ndev = (int)ctx->devs.size();
     uint64_t lo = lower, hi = upper;
     bool have = true;
-    if (ctx->world > 1) {
+    if (ctx->rank_ctx) {
         const Piece mine = slot_pieces(lower, upper, ctx->world, ctx->shares)[(size_t)ctx->rank];
         lo = mine.lo;
         hi = mine.hi;
@@ -445,8 +586,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
     }
     if (have) st.nonces = hi - lo + 1;  // wraps to 0 only for the full 2^64 range
     const std::vector<Piece> pieces =
-        slot_pieces(have ? lo : 1, have ? hi : 0, ndev, ctx->world > 1 ? std::vector<uint32_t>() : ctx->shares);
-    std::vector<std::vector<Launch>> launches(ndev);
+        slot_pieces(have ? lo : 1, have ? hi : 0, ndev, ctx->rank_ctx ? std::vector<uint32_t>() : ctx->shares);
     for (int di = 0; di < ndev; ++di) {
         ctx->devs[di].piece_nonces = pieces[di].lo <= pieces[di].hi ? pieces[di].hi - pieces[di].lo + 1 : 0;
         if (pieces[di].lo > pieces[di].hi) continue;
@@ -484,16 +624,52 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         rc = ensure_counters(ctx->devs[di], launches[di].size());
         if (rc != BM_OK) return rc;
     }
+    return BM_OK;
+}
 
-    // 2-3. enqueue, reduce, combine; a failure part-way drains every stream
-    // first, so the context stays usable
+int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, bm_result_t* out) {
+    const auto t_start = std::chrono::steady_clock::now();
+    bm_stats_t& st = ctx->stats;
+    std::memset(&st, 0, sizeof st);
+    const int ndev = (int)ctx->devs.size();
+    const bool group = ctx->rank_ctx && ctx->joined;
+    if (group && ctx->group_status != BM_OK) {  // the communicator failed earlier: leave the group first
+        st.rccl_status = ctx->group_status;
+        return ctx->group_status;
+    }
+    if (lower > upper) {  // miner.go:45-46 with zero iterations (every rank sees the same range)
+        out->hash = UINT64_MAX;
+        out->nonce = UINT64_MAX;
+        return BM_OK;
+    }
+
+    // 1-2. plan and size every launch; enqueue them and each device's
+    // second-pass reduction.  A failure part-way drains every stream first,
+    // so the context stays usable.
+    std::vector<std::vector<Launch>> launches(ndev);
     std::vector<uint32_t> first(ndev, 0);
-    Partial best;
-    const int rc = enqueue_and_combine(ctx, launches, first, &best);
-    if (rc != BM_OK) {
-        drain(ctx);
-        std::memset(&st, 0, sizeof st);
-        return rc;
+    int rc = plan_launches(ctx, msg, len, lower, upper, launches);
+    if (rc == BM_OK) rc = enqueue(ctx, launches, first);
+    if (rc != BM_OK) drain(ctx);
+
+    // 3. combine (a rank of a group takes part even after a failure)
+    Partial best{UINT64_MAX, UINT64_MAX};
+    if (group) {
+        const int grc = combine_group(ctx, rc, &best);
+        if (grc != BM_OK) {
+            drain(ctx);
+            const int keep = st.rccl_status;
+            std::memset(&st, 0, sizeof st);
+            st.rccl_status = keep;
+            return grc;
+        }
+    } else {
+        if (rc == BM_OK) rc = combine_local(ctx, &best);
+        if (rc != BM_OK) {
+            drain(ctx);
+            std::memset(&st, 0, sizeof st);
+            return rc;
+        }
     }
 
     // 4. balance: the next call's shares follow each device's measured rate
@@ -516,8 +692,16 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
     }
 
     // 5. statistics
+    st.devices = (uint32_t)std::min(ndev, BM_MAX_STAT_DEVICES);
     for (int di = 0; di < ndev; ++di) {
         DeviceCtx& d = ctx->devs[di];
+        if (di < BM_MAX_STAT_DEVICES) {
+            st.dev_nonces[di] = d.piece_nonces;
+            float ms = 0.f;
+            if ((ctx->timing || ctx->balance) && hipSetDevice(d.id) == hipSuccess &&
+                hipEventElapsedTime(&ms, d.bal[0], d.bal[1]) == hipSuccess)
+                st.dev_span_ms[di] = ms;
+        }
         uint32_t li = 0;
         const bool span_ok = ctx->timing && !launches[di].empty() && first[di] < (uint32_t)kEventPairs;
         for (Launch& L : launches[di]) {
@@ -640,6 +824,8 @@ const char* bm_strerror(int status) {
         case BM_ERCCL: return "RCCL error";
         case BM_ENOMEM: return "out of memory";
         case BM_EINTERNAL: return "internal error";
+        case BM_EPEER: return "another rank of the group failed";
+        case BM_ETIMEDOUT: return "the group did not answer within the peer timeout";
         default: return "unknown status";
     }
 }
@@ -726,27 +912,85 @@ int bm_rccl_unique_id(uint8_t* id) {
     return BM_OK;
 }
 
-int bm_ctx_create_rank(int device, int rank, int world, const uint8_t* id, bm_ctx_t** out) {
-    if (!out || !id || world < 1 || rank < 0 || rank >= world) return BM_EINVAL;
+int bm_ctx_create_rank_local(int device, int rank, int world, bm_ctx_t** out) {
+    if (!out || world < 1 || world > BM_MAX_SLOTS || rank < 0 || rank >= world) return BM_EINVAL;
     bm_ctx* ctx = nullptr;
     int rc = bm::create_ctx(&device, 1, world, &ctx);
     if (rc != BM_OK) return rc;
     ctx->rank = rank;
     ctx->world = world;
+    ctx->rank_ctx = true;
+    *out = ctx;
+    return BM_OK;
+}
+
+int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
+    if (!ctx || !id || !ctx->rank_ctx || ctx->joined || timeout_ms < 0) return BM_EINVAL;
+    if (ctx->test_rccl_fault == 1) return BM_ERCCL;  // test hook
     bm::DeviceGuard guard;
+    bm::DeviceCtx& d = ctx->devs[0];
+    if (hipSetDevice(d.id) != hipSuccess) return BM_EHIP;
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
-    if (hipSetDevice(device) != hipSuccess) {
-        bm_ctx_destroy(ctx);
-        return BM_EHIP;
+    // non-blocking, so a group that never forms (a peer that died before
+    // joining) costs timeout_ms, not a hang
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclComm_t comm = nullptr;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+    ncclResult_t r = ncclCommInitRankConfig(&comm, ctx->world, u, ctx->rank, &cfg);
+    int rc = (r == ncclSuccess || r == ncclInProgress) ? BM_OK : BM_ERCCL;
+    if (rc == BM_OK && r == ncclInProgress) rc = bm::comm_settle(comm, r, deadline, timeout_ms > 0);
+    if (rc != BM_OK) {
+        if (comm) (void)ncclCommAbort(comm);
+        return rc;
     }
-    // blocks until every rank of the group has called it
-    if (ncclCommInitRank(&ctx->devs[0].comm, world, u, rank) != ncclSuccess) {
-        ctx->devs[0].comm = nullptr;
-        bm_ctx_destroy(ctx);
-        return BM_ERCCL;
+    d.comm = comm;
+    ctx->joined = true;
+    ctx->group_status = BM_OK;
+    return BM_OK;
+}
+
+int bm_ctx_leave_rank(bm_ctx_t* ctx) {
+    if (!ctx || !ctx->rank_ctx) return BM_EINVAL;
+    bm::DeviceGuard guard;
+    bm::DeviceCtx& d = ctx->devs[0];
+    if (d.comm) {
+        (void)hipSetDevice(d.id);
+        (void)hipStreamSynchronize(d.stream);
+        if (ctx->group_status == BM_OK)
+            (void)ncclCommDestroy(d.comm);
+        else
+            (void)ncclCommAbort(d.comm);
+        d.comm = nullptr;
     }
-    ctx->nccl_ready = true;
+    ctx->joined = false;
+    ctx->group_status = BM_OK;
+    return BM_OK;
+}
+
+int bm_ctx_rank_joined(const bm_ctx_t* ctx, int* joined) {
+    if (!ctx || !joined) return BM_EINVAL;
+    *joined = ctx->joined ? 1 : 0;
+    return BM_OK;
+}
+
+int bm_ctx_set_peer_timeout(bm_ctx_t* ctx, int timeout_ms) {
+    if (!ctx || timeout_ms < 0) return BM_EINVAL;
+    ctx->peer_timeout_ms = timeout_ms;
+    return BM_OK;
+}
+
+int bm_ctx_create_rank(int device, int rank, int world, const uint8_t* id, bm_ctx_t** out) {
+    if (!out || !id) return BM_EINVAL;
+    bm_ctx* ctx = nullptr;
+    int rc = bm_ctx_create_rank_local(device, rank, world, &ctx);
+    if (rc != BM_OK) return rc;
+    rc = bm_ctx_join_rank(ctx, id, 0);  // blocks until every rank of the group has joined
+    if (rc != BM_OK) {
+        bm_ctx_destroy(ctx);
+        return rc;
+    }
     *out = ctx;
     return BM_OK;
 }
@@ -802,9 +1046,14 @@ int bm_reduce_gpu(bm_ctx_t* ctx, const bm_result_t* parts, size_t n, bm_result_t
 }
 
 int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches) {
-    // not for rank contexts: a rank failing alone would leave the others in the allgather
-    if (!ctx || launches < -1 || (ctx->world > 1 && launches >= 0)) return BM_EINVAL;
+    if (!ctx || launches < -1) return BM_EINVAL;
     ctx->fault_after = launches;
+    return BM_OK;
+}
+
+int bm_ctx_set_test_rccl_fault(bm_ctx_t* ctx, int where) {
+    if (!ctx || where < 0 || where > 2) return BM_EINVAL;
+    ctx->test_rccl_fault = where;
     return BM_OK;
 }
 
@@ -834,7 +1083,7 @@ int bm_ctx_set_blocks_per_cu(bm_ctx_t* ctx, int blocks_per_cu) {
 
 int bm_ctx_set_combine(bm_ctx_t* ctx, int mode) {
     if (!ctx || mode < BM_COMBINE_AUTO || mode > BM_COMBINE_HOST) return BM_EINVAL;
-    if (ctx->world > 1 && mode == BM_COMBINE_HOST) return BM_EINVAL;  // ranks combine over RCCL
+    if (ctx->rank_ctx && mode != BM_COMBINE_AUTO) return BM_EINVAL;  // a rank combines through its group
     ctx->combine = mode;
     return BM_OK;
 }
@@ -857,7 +1106,7 @@ int bm_ctx_set_split(bm_ctx_t* ctx, const uint32_t* shares, int n) {
         ctx->shares.clear();
         return BM_OK;
     }
-    const int slots = ctx->world > 1 ? ctx->world : (int)ctx->devs.size();
+    const int slots = ctx->rank_ctx ? ctx->world : (int)ctx->devs.size();
     if (n != slots) return BM_EINVAL;
     for (int i = 0; i < n; ++i)
         if (shares[i] == 0) return BM_EINVAL;
@@ -875,7 +1124,7 @@ int bm_ctx_get_split(const bm_ctx_t* ctx, uint32_t* shares, int cap, int* n) {
 int bm_ctx_set_balance(bm_ctx_t* ctx, int enable) {
     // a rank sees only its own device: a group's shares need an exchange,
     // which is the caller's (the same bm_ctx_set_split on every rank)
-    if (!ctx || (ctx->world > 1 && enable)) return BM_EINVAL;
+    if (!ctx || (ctx->rank_ctx && ctx->world > 1 && enable)) return BM_EINVAL;
     ctx->balance = enable != 0;
     return BM_OK;
 }

@@ -14,9 +14,11 @@ holding the GPU: 8 ranks + 8 sidecars + the launcher exceeded the box's
 16-process guard).  The ranks of one node share a filesystem, so each
 collective is a set of small files: rank r writes `<seq>.<r>` (atomically,
 by rename) and every rank waits until all `world` files of that step exist.
-The directory is keyed by MASTER_ADDR, MASTER_PORT and the launcher's pid (all
-ranks of one torchrun launch share their parent), and rank 0 removes it once
-every rank has left.
+The directory is keyed by MASTER_ADDR, MASTER_PORT, the launcher's pid (all
+ranks of one torchrun launch share their parent) and torchrun's run id and
+restart count (an elastic restart keeps the same parent: its ranks must not
+meet the failed attempt's files), and rank 0 removes it once every rank has
+left.
 
 `all_gather` also carries the partials for the one-GPU rehearsal (every rank
 on device 0, where RCCL cannot place two ranks on one GPU) and for CPU tests.
@@ -35,7 +37,10 @@ class Rendezvous:
         self.rank = int(os.environ["RANK"])
         self.world = int(os.environ["WORLD_SIZE"])
         self.timeout_s = timeout_s
-        key = f"{os.environ.get('MASTER_ADDR', 'local')}-{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}"
+        key = "-".join([os.environ.get("MASTER_ADDR", "local"), os.environ.get("MASTER_PORT", "0"), str(os.getppid()),
+                        os.environ.get("TORCHELASTIC_RUN_ID", "none"),
+                        os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")])
+        key = "".join(ch if ch.isalnum() or ch in "-_." else "_" for ch in key)
         self.path = path or os.environ.get("BTCMINER_RDZV_DIR") or os.path.join(
             tempfile.gettempdir(), f"btcminer-rdzv-{key}")
         os.makedirs(self.path, exist_ok=True)

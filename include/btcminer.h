@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BM_ABI_VERSION 4
+#define BM_ABI_VERSION 5
 
 /* status codes */
 #define BM_OK 0
@@ -50,6 +50,8 @@ extern "C" {
 #define BM_ERCCL (-4)    /* an RCCL call failed (multi-GPU contexts) */
 #define BM_ENOMEM (-5)   /* host or device allocation failed */
 #define BM_EINTERNAL (-6)/* planner invariant violated (a bug) */
+#define BM_EPEER (-7)    /* rank contexts: another rank of the group failed this call */
+#define BM_ETIMEDOUT (-8)/* rank contexts: the group did not answer within the peer timeout */
 
 #define BM_MAX_MSG_LEN (1u << 20) /* bytes; LSP payloads are ~1 KB (README:61) */
 
@@ -86,18 +88,40 @@ int bm_ctx_create(int num_gpus, bm_ctx_t** out);
 int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out);
 
 /* ---- one process per GPU: a context that is one rank of an RCCL group ----
- * Rank 0 calls bm_rccl_unique_id() and hands the bytes to every rank
- * (any side channel: torch.distributed's store, a file, MPI...); each rank
- * then calls bm_ctx_create_rank() on its own device, which blocks until the
- * whole group has joined (ncclCommInitRank).  After that every rank calls
- * bm_search_gpu() with the SAME (msg, lower, upper): rank r scans the r-th
- * of `world` contiguous pieces of the range (near-equal, or per
- * bm_ctx_set_split), and one RCCL
- * allgather of the 16-byte partials gives every rank the result for the
- * whole range.  The reference's equivalent is the server handing each miner
- * a piece of the request (bitcoin/server/server.go:153-169). */
+ * Every rank calls bm_search_gpu() with the SAME (msg, lower, upper): rank r
+ * scans the r-th of `world` contiguous pieces of the range (near-equal, or
+ * per bm_ctx_set_split).  The reference's equivalent is the server handing
+ * each miner a piece of the request (bitcoin/server/server.go:153-169).
+ *
+ * Two steps, so that no rank waits in RCCL for a peer that failed earlier:
+ *   1. bm_ctx_create_rank_local() on the rank's own device: every resource,
+ *      no communicator.  Such a context is usable on its own: a search
+ *      returns THIS rank's partial (its piece's min), which the caller
+ *      combines over any side channel (bench.py's rendezvous gather).
+ *   2. once every rank has created its context (exchange the statuses over
+ *      the side channel), rank 0 calls bm_rccl_unique_id() and hands the
+ *      bytes to every rank, and each calls bm_ctx_join_rank(): a
+ *      non-blocking ncclCommInitRankConfig, polled for at most timeout_ms
+ *      (0: no limit) and aborted after it.  From then on a search ends with
+ *      one RCCL allgather of 32-byte slots {hash, nonce, status, 0}, so
+ *      every rank returns the whole range's answer -- or, when any rank
+ *      failed the call before the combine (it still takes part, with its
+ *      status in the slot), every rank fails it together: the failing rank
+ *      with its own status, the others with BM_EPEER.
+ * bm_ctx_create_rank() is both steps in one call (blocking join).
+ * bm_ctx_set_peer_timeout(): a joined rank waits at most this long for the
+ *   group's allgather after its own work ends (0, the default: no limit);
+ *   past it the communicator is aborted and the call returns BM_ETIMEDOUT,
+ *   as does every later search until bm_ctx_leave_rank().
+ * bm_ctx_leave_rank(): drop the communicator; searches return the rank's
+ *   own partial again.  bm_ctx_rank_joined(): 1 inside a group, else 0. */
 #define BM_RCCL_ID_BYTES 128
 int bm_rccl_unique_id(uint8_t* id /* BM_RCCL_ID_BYTES */);
+int bm_ctx_create_rank_local(int device, int rank, int world, bm_ctx_t** out);
+int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms);
+int bm_ctx_leave_rank(bm_ctx_t* ctx);
+int bm_ctx_rank_joined(const bm_ctx_t* ctx, int* joined);
+int bm_ctx_set_peer_timeout(bm_ctx_t* ctx, int timeout_ms);
 int bm_ctx_create_rank(int device, int rank, int world, const uint8_t* id, bm_ctx_t** out);
 int bm_ctx_rank(const bm_ctx_t* ctx, int* rank, int* world);
 int bm_ctx_destroy(bm_ctx_t* ctx);
@@ -133,6 +157,13 @@ typedef struct bm_launch_stat {
                              library built with BM_CLOCK_PROBE=1; 0 otherwise) */
 } bm_launch_stat_t;
 
+/* How the last search combined its partials (bm_stats_t.combine_used). */
+#define BM_COMBINED_NONE 0  /* nothing to combine (empty range) */
+#define BM_COMBINED_RCCL 1  /* one RCCL allgather (the devices of the context, or the ranks of its group) */
+#define BM_COMBINED_HOST 2  /* device-to-host copies of every device's partial */
+#define BM_COMBINED_LOCAL 3 /* a rank context outside a group: this rank's own partial */
+#define BM_MAX_STAT_DEVICES 16
+
 typedef struct bm_stats {
     uint32_t launches;     /* search-kernel launches of the last call */
     uint32_t recorded;     /* entries filled in launch[] (<= BM_MAX_LAUNCH_STATS) */
@@ -141,7 +172,15 @@ typedef struct bm_stats {
                               different streams overlap, so this can exceed span_ms */
     double span_ms;        /* first launch's start to the last launch's end on
                               one device (timing on; max over devices) */
-    uint64_t nonces;       /* nonces in the last call */
+    uint64_t nonces;       /* nonces this process scanned in the last call */
+    int32_t combine_used;  /* BM_COMBINED_*: how the partials were combined */
+    int32_t rccl_status;   /* the RCCL failure this context fell back from or
+                              stopped on (BM_ERCCL / BM_ETIMEDOUT), 0 if none */
+    uint32_t devices;      /* entries of dev_nonces / dev_span_ms */
+    uint32_t reserved;
+    uint64_t dev_nonces[BM_MAX_STAT_DEVICES];  /* nonces each device of the context scanned */
+    double dev_span_ms[BM_MAX_STAT_DEVICES];   /* each device's first operation to the end of
+                                                  its reduction (timing on) */
     bm_launch_stat_t launch[BM_MAX_LAUNCH_STATS];
 } bm_stats_t;
 
@@ -168,10 +207,15 @@ int bm_ctx_set_max_windows(bm_ctx_t* ctx, int max_windows);
 int bm_ctx_set_task_digits(bm_ctx_t* ctx, int digits);
 
 /* How a context combines its per-device 16-byte partials:
- * BM_COMBINE_AUTO (default): RCCL allgather when the context has > 1 device,
- * a plain device-to-host copy otherwise; BM_COMBINE_RCCL: always RCCL (also
- * for one device: exercises the collective path on a single GPU);
- * BM_COMBINE_HOST: device-to-host copies of every partial, no RCCL. */
+ * BM_COMBINE_AUTO (default): RCCL allgather when the context has > 1
+ * distinct device, a plain device-to-host copy otherwise; BM_COMBINE_RCCL:
+ * always RCCL (also for one device: exercises the collective path on a
+ * single GPU; BM_EINVAL on a context that lists a device twice);
+ * BM_COMBINE_HOST: device-to-host copies of every partial, no RCCL.
+ * When RCCL fails at run time (ncclCommInitAll or the allgather), the
+ * context aborts its communicators, combines that call and every later one
+ * by host copies, and reports it: combine_used = BM_COMBINED_HOST,
+ * rccl_status = BM_ERCCL.  The answer is the same either way. */
 #define BM_COMBINE_AUTO 0
 #define BM_COMBINE_RCCL 1
 #define BM_COMBINE_HOST 2
@@ -217,10 +261,17 @@ int bm_reduce_gpu(bm_ctx_t* ctx, const bm_result_t* parts, size_t n, bm_result_t
 
 /* Make every later bm_search_gpu fail with BM_EINTERNAL after enqueueing
  * `launches` search launches (-1: off).  Exercises the failure path: the
- * call drains what it queued and the context stays usable.  BM_EINVAL on a
- * rank context of more than one rank (one rank failing alone would leave the
- * others waiting in the allgather). */
+ * call drains what it queued and the context stays usable.  On a joined
+ * rank context the failure reaches the whole group through the status word
+ * of the allgather (the others return BM_EPEER). */
 int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches);
+
+/* Make RCCL fail on purpose (0: off): 1 = the next communicator set-up
+ * (ncclCommInitAll, or bm_ctx_join_rank), 2 = every allgather, before it is
+ * enqueued.  A multi-device context then falls back to host copies; a
+ * joined rank context fails the call (at world 1 only: a real group's peers
+ * would wait for it until their peer timeout). */
+int bm_ctx_set_test_rccl_fault(bm_ctx_t* ctx, int where);
 
 /* ---- host-side plan introspection (pure CPU; used by the CPU tests) ---- */
 

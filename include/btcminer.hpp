@@ -64,6 +64,17 @@ class Context {
         check(bm_ctx_create_rank(device, rank, world, id, &c.ctx_), "bm_ctx_create_rank");
         return c;
     }
+    // rank `rank` of `world` outside a group: search() returns this rank's
+    // partial; join() then makes it a member of the RCCL group
+    static Context rank_local(int device, int rank, int world) {
+        Context c{Empty{}};
+        check(bm_ctx_create_rank_local(device, rank, world, &c.ctx_), "bm_ctx_create_rank_local");
+        return c;
+    }
+    void join(const uint8_t (&id)[BM_RCCL_ID_BYTES], int timeout_ms = 0) {
+        check(bm_ctx_join_rank(ctx_, id, timeout_ms), "bm_ctx_join_rank");
+    }
+    void leave() { check(bm_ctx_leave_rank(ctx_), "bm_ctx_leave_rank"); }
     Context(Context&& o) noexcept : ctx_(std::exchange(o.ctx_, nullptr)) {}
     Context& operator=(Context&& o) noexcept {
         if (this != &o) {

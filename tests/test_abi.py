@@ -32,8 +32,8 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     lib = _lib.load()
-    assert lib.bm_abi_version() == _lib.BM_ABI_VERSION == 4
-    for code in range(0, -7, -1):
+    assert lib.bm_abi_version() == _lib.BM_ABI_VERSION == 5
+    for code in range(0, -9, -1):
         assert lib.bm_strerror(code).decode() != "unknown status"
     assert lib.bm_strerror(-99).decode() == "unknown status"
 
@@ -52,6 +52,13 @@ def test_invalid_arguments_rejected():
     for dev, rank, world in [(0, 0, 0), (0, 2, 2), (0, -1, 2)]:
         assert lib.bm_ctx_create_rank(dev, rank, world, uid, ctypes.byref(h)) == _lib.BM_EINVAL
     assert lib.bm_ctx_create_rank(0, 0, 1, None, ctypes.byref(h)) == _lib.BM_EINVAL
+    for dev, rank, world in [(0, 0, 0), (0, 2, 2), (0, -1, 2), (0, 0, 1025)]:
+        assert lib.bm_ctx_create_rank_local(dev, rank, world, ctypes.byref(h)) == _lib.BM_EINVAL
+    assert lib.bm_ctx_join_rank(None, uid, 0) == _lib.BM_EINVAL
+    assert lib.bm_ctx_leave_rank(None) == _lib.BM_EINVAL
+    assert lib.bm_ctx_rank_joined(None, ctypes.byref(n)) == _lib.BM_EINVAL
+    assert lib.bm_ctx_set_peer_timeout(None, 10) == _lib.BM_EINVAL
+    assert lib.bm_ctx_set_test_rccl_fault(None, 1) == _lib.BM_EINVAL
     assert lib.bm_reduce_gpu(None, None, 0, ctypes.byref(r)) == _lib.BM_EINVAL
     assert lib.bm_ctx_set_test_fault(None, 0) == _lib.BM_EINVAL
     assert lib.bm_ctx_rank(None, ctypes.byref(n), ctypes.byref(n)) == _lib.BM_EINVAL
@@ -64,6 +71,32 @@ def test_invalid_arguments_rejected():
     assert lib.bm_device_pci_bus_id(-1, buf, 64) == _lib.BM_ENODEV
 
 
+def test_stats_layout_matches_the_header():
+    """The ctypes mirrors of bm_stats_t / bm_launch_stat_t / bm_segment_t
+    have the C layout: sizes and every field offset, from a C program
+    compiled against include/btcminer.h (a misread stats block would
+    mislabel nonces and rates in bench.py)."""
+    import subprocess
+    import tempfile
+    structs = {"bm_stats_t": _lib.Stats, "bm_launch_stat_t": _lib.LaunchStat, "bm_segment_t": _lib.Segment}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "btcminer.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _t in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines += ["return 0;", "}"]
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "layout.c"), os.path.join(d, "layout")
+        open(src, "w").write("\n".join(lines) + "\n")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), src, "-o", exe])
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = {tuple(ln.split()[:2]): int(ln.split()[2]) for ln in out if ln.strip()}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f, _t in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
 @pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")
 def test_no_gpu_fails_loudly():
     with pytest.raises(_lib.BtcMinerError) as ei:
@@ -71,6 +104,9 @@ def test_no_gpu_fails_loudly():
     assert ei.value.status == _lib.BM_ENODEV
     with pytest.raises(_lib.BtcMinerError) as ei:
         _lib.Context(devices=[0], rank=0, world=1, unique_id=b"\0" * _lib.BM_RCCL_ID_BYTES)
+    assert ei.value.status == _lib.BM_ENODEV
+    with pytest.raises(_lib.BtcMinerError) as ei:
+        _lib.Context(devices=[0], rank=1, world=2)
     assert ei.value.status == _lib.BM_ENODEV
 
 

@@ -228,7 +228,8 @@ def test_cpp_gpu_miner_in_the_system(oracle):
 
 
 @pytest.mark.gpu
-def test_c5_native_at_size():
+@pytest.mark.parametrize("cfg", ["C5"])
+def test_c5_native_at_size(cfg):
     """BASELINE C5 at full size with every process native: the C++ server,
     4 C++ GPU miners on device 0, 16 C++ clients asking for [0, 2^34-1] of
     "client-%02d", 2^32-nonce jobs, 10% read and write drop at every endpoint

@@ -160,3 +160,27 @@ def test_torch_gloo_combine_equals_single_scan(oracle, world):
             p.join(timeout=60)
             assert p.exitcode == 0
         assert all(res == oracle.search(msg, lo, hi) for _, res in out), out
+
+
+def test_rendezvous_key_separates_elastic_restarts(tmp_path, monkeypatch):
+    """a torchrun elastic restart keeps the agent (the parent pid)
+    and the master address and port, so the rendezvous directory is also keyed
+    by the run id and the restart count: a restarted group never meets the
+    failed attempt's files."""
+    from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    monkeypatch.delenv("BTCMINER_RDZV_DIR", raising=False)
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    import tempfile
+    monkeypatch.setattr(tempfile, "tempdir", str(tmp_path))
+    paths = []
+    for run_id, restart in (("abc", "0"), ("abc", "1"), ("xyz/1", "0")):
+        monkeypatch.setenv("TORCHELASTIC_RUN_ID", run_id)
+        monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", restart)
+        with Rendezvous(timeout_s=10) as rz:
+            paths.append(rz.path)
+            assert rz.all_gather(7) == [7]
+    assert len(set(paths)) == 3 and all(os.path.dirname(p) == str(tmp_path) for p in paths)

@@ -126,7 +126,8 @@ def test_c4_random_windows(gpu_ctx):
         assert gpu_ctx.search(d["msg"].encode(), w["lower"], w["upper"]) == (w["hash"], w["nonce"]), w
 
 
-def test_c4_whole_range():
+@pytest.mark.parametrize("cfg", ["C4"])
+def test_c4_whole_range(cfg):
     """C4 itself, [0, 2^40-1], through every visible device of one context
     (one GPU here: ~20 s), against the golden from 256 oracle chunks."""
     d = _scale()
@@ -371,3 +372,148 @@ def test_bench_rehearsals_balance_after_warmup():
     sp = out["config"]["split"]
     assert out["result_ok"] is True and sp["mode"].startswith("measured rank rates"), sp
     assert len(sp["shares"]) == 2 and max(sp["shares"]) == 65536
+
+
+# ---- fail-safe combines (ABI 5) ---------------------------------------------
+
+from distributed_bitcoin_minter_amd._lib import (BM_COMBINED_HOST, BM_COMBINED_LOCAL,  # noqa: E402
+                                                 BM_COMBINED_RCCL, BM_ERCCL, BM_ETIMEDOUT)
+
+
+@pytest.mark.parametrize("where", [1, 2])
+def test_rccl_failure_falls_back_to_host_copies(oracle, where):
+    """A one-process context whose RCCL combine fails (1: ncclCommInitAll,
+    2: the grouped allgather; forced by the test hook) aborts its
+    communicators and combines by host copies -- the same answer, reported
+    as combine_used = host with rccl_status = BM_ERCCL, for that call and
+    every later one."""
+    msg, lo, hi = b"bradfitz", 999_000_000, 1_000_999_999
+    want = oracle.search(msg, lo, hi, threads=8)
+    with Context(devices=[0]) as c:
+        c.set_combine(BM_COMBINE_RCCL)
+        assert c.search(msg, lo, hi) == want
+        st = c.last_stats()
+        assert (st.combine_used, st.rccl_status) == (BM_COMBINED_RCCL, 0)
+    with Context(devices=[0]) as c:
+        c.set_combine(BM_COMBINE_RCCL)
+        c.set_test_rccl_fault(where)
+        for _ in range(2):
+            assert c.search(msg, lo, hi) == want
+            st = c.last_stats()
+            assert (st.combine_used, st.rccl_status) == (BM_COMBINED_HOST, BM_ERCCL)
+        c.set_test_rccl_fault(0)
+        assert c.search(bytes.fromhex(C2["msg_hex"]), C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
+        assert c.last_stats().combine_used == BM_COMBINED_HOST  # stays on host copies
+
+
+def test_rank_contexts_outside_a_group(oracle):
+    """the rank path of the library at world > 1 without a
+    communicator.  Three rank contexts (ranks 0-2 of 3) on GPU 0 each scan
+    exactly their bm_split_range piece -- near-equal, with shares 1:2:5, and
+    for a range shorter than the group -- return their own partial
+    (combine_used = local), and the lexicographic min of the three equals
+    the oracle and the C2 golden."""
+    from distributed_bitcoin_minter_amd import _lib
+    from distributed_bitcoin_minter_amd.dist import lex_min
+    msg = b"bradfitz"
+    ctxs = [Context(devices=[0], rank=r, world=3) for r in range(3)]
+    try:
+        assert all(not c.joined() and c.rank() == (r, 3) for r, c in enumerate(ctxs))
+        for shares in (None, [1, 2, 5]):
+            for c in ctxs:
+                c.set_split(shares)
+            for lo, hi in [(0, 9999), (999_999_000, 1_000_001_000), (U64 - 5000, U64), (7, 8), (5, 5),
+                           (C2["lower"], C2["upper"])]:
+                pieces = _lib.split_range(lo, hi, 3, shares)
+                parts = []
+                for r, c in enumerate(ctxs):
+                    parts.append(c.search(msg, lo, hi))
+                    st = c.last_stats()
+                    assert st.nonces == (0 if pieces[r] is None else pieces[r][1] - pieces[r][0] + 1), (shares, lo, r)
+                    assert st.combine_used == BM_COMBINED_LOCAL
+                    want_r = oracle.search(msg, *pieces[r], threads=8) if pieces[r] and hi - lo < 10 ** 7 else None
+                    if pieces[r] is None:
+                        assert parts[-1] == (U64, U64)
+                    elif want_r is not None:
+                        assert parts[-1] == want_r, (shares, lo, r)
+                got = lex_min(parts)
+                if (lo, hi) == (C2["lower"], C2["upper"]):
+                    assert got == (C2["hash"], C2["nonce"])
+                else:
+                    assert got == oracle.search(msg, lo, hi, threads=8), (shares, lo, hi)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_rank_group_world1_status_and_leave(oracle):
+    """A joined rank context (world 1 on this box) combines through the
+    status-carrying allgather: a failure before the combine comes back as the
+    rank's own status; an allgather failure (test hook) aborts the
+    communicator and every later search returns BM_ERCCL until leave(); after
+    leave() the context answers with its own partial; a fresh join works."""
+    msg, lo, hi = b"bradfitz", 999_000_000, 1_000_999_999
+    want = oracle.search(msg, lo, hi, threads=8)
+    with Context(devices=[0], rank=0, world=1) as c:
+        c.join(rccl_unique_id(), timeout_ms=60_000)
+        assert c.joined()
+        c.set_peer_timeout(60_000)
+        assert c.search(msg, lo, hi) == want and c.last_stats().combine_used == BM_COMBINED_RCCL
+        for fault in (0, 1):
+            c.set_test_fault(fault)
+            with pytest.raises(BtcMinerError) as ei:
+                c.search(msg, lo, hi)
+            assert ei.value.status == BM_EINTERNAL
+        c.set_test_fault(-1)
+        assert c.search(msg, lo, hi) == want                   # the group survived a rank-side failure
+        c.set_test_rccl_fault(2)
+        for _ in range(2):
+            with pytest.raises(BtcMinerError) as ei:
+                c.search(msg, lo, hi)
+            assert ei.value.status == BM_ERCCL
+        c.set_test_rccl_fault(0)
+        with pytest.raises(BtcMinerError) as ei:               # the communicator is gone
+            c.search(msg, lo, hi)
+        assert ei.value.status == BM_ERCCL
+        c.leave()
+        assert not c.joined()
+        assert c.search(msg, lo, hi) == want and c.last_stats().combine_used == BM_COMBINED_LOCAL
+        c.join(rccl_unique_id())
+        assert c.search(bytes.fromhex(C2["msg_hex"]), C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
+        c.leave()
+        c.set_test_rccl_fault(1)
+        with pytest.raises(BtcMinerError) as ei:
+            c.join(rccl_unique_id())
+        assert ei.value.status == BM_ERCCL and not c.joined()
+
+
+def test_join_without_peers_times_out():
+    """Rank 0 of 2 joining a group whose other rank never comes: the
+    non-blocking ncclCommInitRankConfig is polled for timeout_ms, then
+    aborted -- BM_ETIMEDOUT instead of a hang -- and the context still
+    searches its own piece."""
+    import time
+    with Context(devices=[0], rank=0, world=2) as c:
+        t = time.monotonic()
+        with pytest.raises(BtcMinerError) as ei:
+            c.join(rccl_unique_id(), timeout_ms=3000)
+        assert ei.value.status in (BM_ETIMEDOUT, BM_ERCCL) and time.monotonic() - t < 60
+        assert not c.joined()
+        assert c.search(b"msg", 0, 3) == (4754799531757243342, 1)  # rank 0's piece of [0, 3]: [0, 1]
+
+
+def test_bench_torchrun_with_per_rank_visibility_mask():
+    """a launcher that gives every rank a one-device visibility
+    mask.  Two torchrun ranks with HIP_VISIBLE_DEVICES=0 (LOCAL_RANK 0 and 1)
+    both drive their one visible device; RCCL refuses the shared GPU, so the
+    ranks agree to gather their partials over the rendezvous instead.  The
+    line names that combine, and each rank's nonces, which add up to the
+    workload; the answer equals the weak2 golden."""
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="0")
+    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], env=env, torchrun=2))
+    assert out["result_ok"] is True and out["n_gpus"] == 2
+    cfg = out["config"]
+    assert "rendezvous gather" in cfg["parallelism"] and "RCCL group failed" in cfg["parallelism"], cfg
+    ranks = sorted(cfg["ranks"], key=lambda r: r["rank"])
+    assert [r["device"] for r in ranks] == [0, 0] and all(r["combine"] == "local" for r in ranks)
+    assert sum(r["nonces"] for r in ranks) == cfg["global_nonces"]

@@ -93,7 +93,8 @@ def test_c5_gpu_miners_16_clients_10pct_drop(gpu_ctx, oracle):
     stop(bs, threads, gm)
 
 
-def test_c5_at_size_against_cpu_goldens():
+@pytest.mark.parametrize("cfg", ["C5"])
+def test_c5_at_size_against_cpu_goldens(cfg):
     """BASELINE C5 at its full size: 16 clients, each asking for [0, 2^34-1]
     of "client-%02d", 2^32-nonce jobs (the server default), 4 GPU miners
     sharing the box's GPU, 10% read and write drop at every endpoint.
@@ -154,7 +155,8 @@ def test_gpu_miner_failover():
     stop(bs, threads, gm)
 
 
-def test_c1_all_processes():
+@pytest.mark.parametrize("cfg", ["C1"])
+def test_c1_all_processes(cfg):
     """./server, ./miner (GPU) and ./client as separate processes; the
     client's stdout is matched like the reference's graders did."""
     import subprocess
