@@ -45,7 +45,7 @@ for phase in "$@"; do
         -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
       step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run \
         -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
-    parity) step parity_campaign 600 python -u tools/parity_campaign.py --cases 3000 --seed 303 ;;
+    parity) step parity_campaign 600 python -u tools/parity_campaign.py 3000 303 ;;
     *) echo "unknown phase $phase"; exit 2 ;;
   esac
 done
