@@ -525,13 +525,19 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
     if (ctx->test_rccl_fault == 2) {
         rc = BM_ERCCL;  // test hook: as if the allgather failed (world 1 only: no peer is left waiting)
     } else {
-        if (hipEventSynchronize(d.own_done) != hipSuccess) return BM_EHIP;  // own work: no deadline
-        const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ctx->peer_timeout_ms);
+        // the allgather goes on the stream behind this rank's own work (a
+        // non-blocking communicator may first report ncclInProgress: then it
+        // is enqueued once the communicator settles)
+        const auto timeout = std::chrono::milliseconds(ctx->peer_timeout_ms);
         rc = comm_settle(d.comm, ncclAllGather(d.d_slot, d.d_gather, kSlotWords, ncclUint64, d.comm, d.stream),
-                         deadline, limited);
+                         std::chrono::steady_clock::now() + timeout, limited);
         if (rc == BM_OK && hipMemcpyAsync(d.h_slots, d.d_gather, sizeof(Slot) * world, hipMemcpyDeviceToHost,
                                           d.stream) != hipSuccess)
             return BM_EHIP;
+        // the deadline counts from the end of this rank's own work: only the
+        // wait for the other ranks is bounded
+        if (hipEventSynchronize(d.own_done) != hipSuccess) return BM_EHIP;
+        const auto deadline = std::chrono::steady_clock::now() + timeout;
         if (rc == BM_OK && !limited) {
             if (hipStreamSynchronize(d.stream) != hipSuccess) return BM_EHIP;
         } else if (rc == BM_OK) {
@@ -544,7 +550,7 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
                     break;
                 }
                 std::this_thread::sleep_for(pause);
-                pause = std::min(pause * 2, std::chrono::microseconds(1000));
+                pause = std::min(pause * 2, std::chrono::microseconds(100));
             }
         }
     }

@@ -74,3 +74,108 @@ def test_bench_imports_no_torch():
     mods = {a.name.split(".")[0] for n in ast.walk(tree) if isinstance(n, ast.Import) for a in n.names}
     mods |= {n.module.split(".")[0] for n in ast.walk(tree) if isinstance(n, ast.ImportFrom) and n.module}
     assert "torch" not in mods
+
+
+# bench.py's torchrun rank set-up (open_contexts) at world > 1, on CPU: the
+# library's Context is replaced by a stand-in whose search is the oracle's
+# scan of the rank's piece (a rank context outside a group returns its own
+# partial), so the agreement logic over the file rendezvous -- all ranks
+# create, all join or all fall back to the rendezvous gather, a failed
+# creation stops every rank -- runs for real, with real processes.
+_RANK_SETUP = r"""
+import json, os, sys, types
+root = sys.argv[1]
+sys.path[:0] = [root, os.path.join(root, "tests")]
+import bench
+from conftest import Oracle
+from distributed_bitcoin_minter_amd import _lib
+from distributed_bitcoin_minter_amd.dist import rank_piece
+oracle = Oracle(os.path.join(root, "oracle", "liboracle.so"))
+fail = os.environ.get("FAKE_FAIL", "")          # "create:<rank>" or "join:<rank>"
+U64 = 2**64 - 1
+
+class FakeCtx:
+    def __init__(self, devices=None, rank=None, world=None, **kw):
+        self.rank_, self.world_, self.dev, self._joined, self.shares = rank, world, devices[0], False, None
+        if fail == f"create:{rank}":
+            raise _lib.BtcMinerError(_lib.BM_EHIP, "bm_ctx_create_rank_local")
+    def join(self, uid, timeout_ms=0):
+        if fail == f"join:{self.rank_}":
+            raise _lib.BtcMinerError(_lib.BM_ETIMEDOUT, "bm_ctx_join_rank")
+        self._joined = True
+    def joined(self): return self._joined
+    def leave(self): self._joined = False
+    def set_peer_timeout(self, ms): self.timeout = ms
+    def set_split(self, s): self.shares = s
+    def close(self): pass
+    def search(self, msg, lo, hi):
+        piece = rank_piece(lo, hi, self.rank_, self.world_, self.shares)
+        part = oracle.search(msg, *piece) if piece else (U64, U64)
+        if self._joined:   # the in-library allgather: stand in with the whole range
+            return oracle.search(msg, lo, hi)
+        return part
+
+bench.Context = FakeCtx
+bench.device_count = lambda: 1
+bench.rccl_unique_id = lambda: os.urandom(128)
+args = types.SimpleNamespace(rehearse_one_gpu=False, combine=os.environ.get("COMBINE", "rccl"))
+ctx, grp, search, how, dev = bench.open_contexts(args, int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"]),
+                                                 int(os.environ["LOCAL_RANK"]))
+res = search(b"bradfitz", 0, 99_999)
+grp.close()
+print(json.dumps({"rank": grp.rank, "how": how, "dev": dev, "joined": ctx.joined(), "res": list(res)}))
+"""
+
+
+def _rank_setup(world, **env_extra):
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE=str(world), **env_extra)
+        procs.append(subprocess.Popen([sys.executable, "-c", _RANK_SETUP, ROOT], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=120)
+        outs.append((p.returncode, o, e))
+    return outs
+
+
+def test_bench_ranks_join_together(oracle):
+    want = list(oracle.search(b"bradfitz", 0, 99_999))
+    outs = _rank_setup(3)
+    import json
+    res = [json.loads(o.strip().splitlines()[-1]) for rc, o, e in outs if rc == 0]
+    assert len(res) == 3, [e[-2000:] for _, _, e in outs]
+    assert all(r["joined"] and "RCCL allgather" in r["how"] and r["res"] == want for r in res)
+    assert all(r["dev"] == 0 for r in res)  # one visible device per rank (a visibility mask): device 0
+
+
+def test_bench_ranks_fall_back_together_when_one_join_fails(oracle):
+    """One rank's join fails (here: rank 1 times out): every rank leaves the
+    group and the partials meet over the rendezvous; the line says why."""
+    import json
+    want = list(oracle.search(b"bradfitz", 0, 99_999))
+    outs = _rank_setup(3, FAKE_FAIL="join:1")
+    res = [json.loads(o.strip().splitlines()[-1]) for rc, o, e in outs if rc == 0]
+    assert len(res) == 3, [e[-2000:] for _, _, e in outs]
+    for r in res:
+        assert not r["joined"] and r["res"] == want
+        assert "rendezvous gather" in r["how"] and "RCCL group failed: rank 1" in r["how"], r["how"]
+    outs = _rank_setup(2, COMBINE="gather")
+    res = [json.loads(o.strip().splitlines()[-1]) for rc, o, e in outs if rc == 0]
+    assert len(res) == 2 and all("--combine gather" in r["how"] and r["res"] == want for r in res)
+
+
+def test_bench_ranks_stop_together_when_one_context_fails():
+    """A rank whose context cannot be created stops every rank (exit 1, the
+    failing rank named) before any of them joins RCCL: no rank is left
+    waiting in a communicator for it."""
+    outs = _rank_setup(3, FAKE_FAIL="create:2")
+    assert [rc for rc, _, _ in outs] == [1, 1, 1], outs
+    assert all("rank 2" in e for _, _, e in outs)

@@ -1,9 +1,24 @@
 #!/bin/bash
-# The GPU checks of a round, in one gpurun call; each phase named on the
-# command line runs under its own time limit, and the script stops at the
-# first phase that faults, aborts or times out (gpurun rules).
-#   tools/gpu_round.sh smoke tests bench
-#   phases: smoke | tests | tests_multi | bench | bench_c3 | bench_c4 | rehearse | prof | pmc | parity
+# Every GPU check of a round, in one gpurun call.  Each phase named on the
+# command line runs under its own time limit; the script stops at the first
+# phase that faults, aborts or times out (gpurun rules: nothing more runs on
+# the GPU after such a step).
+#
+#   /usr/local/graft/bin/gpurun -- 'bash tools/gpu_round.sh smoke tests bench'
+#
+# phases:
+#   driver      what the driver runs at round end, in its words (pytest -x -q -m gpu, smoke(), bench.py)
+#   smoke       __graft_entry__.smoke()
+#   tests       the whole GPU suite (config-tagged parity tests first, tests/conftest.py)
+#   tests_multi tests/test_gpu_multi.py only
+#   bench       C2 bench line, 20 steps (the driver's N = 1 line); bench_c3, bench_c4: C3 / C4 on one GPU
+#   rehearse    the multi-GPU modes on one GPU: one process 2-way split, 2 torchrun ranks under a
+#               per-rank visibility mask, C4 over 8 one-process slots
+#   c5          C5 at size: the native (C++) system and the Python one
+#   prof        rocprofv3 kernel traces of C2 (2 streams, 1 stream) and C3
+#   pmc         PMC passes (FETCH_SIZE, WRITE_SIZE, SQ) for C2 and C3, one counter group per run
+#   parity      tools/parity_campaign.py, 3,000 random cases
+#   ab          A/B of library variants: AB_LIBS="a.so b.so" (parity of each first, then alternating)
 # Logs and profiles land in gpurun_out/$TAG (TAG defaults to r03).
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
@@ -19,33 +34,55 @@ step() {  # name, seconds, command...
   # 1 = test failures / a wrong answer: reported, the next phase still runs;
   # anything else (fault, abort, timeout, signal) ends the call here
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
-  return 0
+  return $rc
 }
 PYTEST="python -u -m pytest -p no:cacheprovider --timeout 300 --timeout-method thread -rs"
+BENCH="python3 bench.py --no-cpu-baseline"
+D=distributed_bitcoin_minter_amd
 for phase in "$@"; do
   case $phase in
+    driver)
+      step driver_tests 1200 python -m pytest tests/ -x -q -m gpu
+      step driver_smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
+      step driver_bench 400 python bench.py ;;
     smoke) step smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step gpu_tests 1000 $PYTEST tests -m gpu -v ;;
+    tests) step gpu_tests 1200 $PYTEST tests -m gpu -v ;;
     tests_multi) step gpu_tests_multi 600 $PYTEST tests/test_gpu_multi.py -m gpu -v ;;
     bench) step bench_C2 300 python -u bench.py --steps 20 --warmup 5 ;;
-    bench_c3) step bench_C3 300 python -u bench.py --config C3 --steps 20 --warmup 5 --no-cpu-baseline ;;
-    bench_c4) step bench_C4 300 python -u bench.py --config C4 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    bench_c3) step bench_C3 300 $BENCH --config C3 --steps 20 --warmup 5 ;;
+    bench_c4) step bench_C4 300 $BENCH --config C4 --steps 2 --warmup 1 ;;
     rehearse)
-      step rehearse2_oneproc 300 python -u bench.py --gpus 2 --steps 3 --warmup 2 --no-cpu-baseline --rehearse-one-gpu
-      step rehearse2_mask 300 env HIP_VISIBLE_DEVICES=0 python -u -m torch.distributed.run --nnodes=1 \
-        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 2 ;;
+      step rehearse2_oneproc 300 $BENCH --gpus 2 --steps 3 --warmup 2 --rehearse-one-gpu
+      step rehearse2_mask 400 env HIP_VISIBLE_DEVICES=0 python -u -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 2
+      step rehearse8_C4 300 $BENCH --config C4 --gpus 8 --rehearse-one-gpu --steps 1 --warmup 1 ;;
+    c5)
+      step c5_native 300 python -u tools/bench_c5_native.py
+      step c5_python 300 python -u tools/bench_c5.py ;;
     prof)
-      # 1-stream kernel trace of the C2 bench (the dominant launch alone on its stream)
-      step prof_C2 300 env BTCMINER_STREAMS=1 rocprofv3 --kernel-trace --stats -d "$OUT/prof_C2" -o run \
-        -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+      step prof_C2 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_C2" -o run --output-format csv -- $BENCH --steps 5 --warmup 2
+      step prof_C2_1stream 300 env BTCMINER_STREAMS=1 rocprofv3 --kernel-trace --stats -d "$OUT/prof_C2_1stream" -o run \
+        --output-format csv -- $BENCH --steps 5 --warmup 2
+      step prof_C3 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_C3" -o run --output-format csv -- $BENCH --config C3 \
+        --steps 5 --warmup 2 ;;
     pmc)
-      step pmc_sq 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_WAVES GRBM_GUI_ACTIVE -d "$OUT/pmc_sq" -o run \
-        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
-      step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run \
-        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
-      step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run \
-        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+      for C in C2 C3; do
+        step pmc_${C}_fetch 90 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_${C}_fetch" -o f --output-format csv \
+          -- python3 tools/prof_one.py $C 2
+        step pmc_${C}_write 90 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_${C}_write" -o w --output-format csv \
+          -- python3 tools/prof_one.py $C 2
+        step pmc_${C}_sq 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+          SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE -d "$OUT/pmc_${C}_sq" -o s --output-format csv \
+          -- python3 tools/prof_one.py $C 2
+      done ;;
     parity) step parity_campaign 600 python -u tools/parity_campaign.py 3000 303 ;;
+    ab)
+      for lib in $AB_LIBS; do
+        n=$(basename "$lib" .so)
+        BTCMINER_LIB=$PWD/$lib step "parity_$n" 300 $PYTEST tests/test_gpu_parity.py -q -x || { echo "parity $n failed"; exit 1; }
+      done
+      L="$D/libbtcminer.so $AB_LIBS"
+      step ab 1200 env AB_REPS=${AB_REPS:-5} python -u tools/ab_bench.py $L $L $L $L ;;
     *) echo "unknown phase $phase"; exit 2 ;;
   esac
 done

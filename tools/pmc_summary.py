@@ -27,6 +27,7 @@ for f in glob.glob(os.path.join(src, f"pmc_{cfg}_*" if cfg else "pmc_*", "*_coun
         d = (tag, r["Dispatch_Id"])
         per[k][d][r["Counter_Name"]] = per[k][d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         dur[k][d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+MIN_CLOCK_S = 0.005  # clock only from launches at least this long
 res = {}
 for k, disp in per.items():
     if "search_kernel" not in k:
@@ -47,10 +48,14 @@ for k, disp in per.items():
     e = {"counters": {c: v for c, v in m.items() if not c.startswith("_")}, "duration_ms": m["_dur_s"] * 1e3}
     if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
         e["hbm_bytes_per_launch"] = int((m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024)
-    if "GRBM_GUI_ACTIVE" in m:
+    if "GRBM_GUI_ACTIVE" in m and m["_dur_s"] >= MIN_CLOCK_S:
         e["clock_ghz"] = m["GRBM_GUI_ACTIVE"] / 8 / m["_dur_s"] / 1e9
         if "SQ_INSTS_VALU" in m:
             e["simd_cycles_per_valu"] = (m["GRBM_GUI_ACTIVE"] / 8) * 1024 / m["SQ_INSTS_VALU"]
+    elif "GRBM_GUI_ACTIVE" in m:
+        # GRBM_GUI_ACTIVE counts the busy cycles of the whole counter window,
+        # not only the kernel's: over a launch of a few ms it gave 2.7-6.9 GHz
+        e["clock_note"] = f"no clock: launch shorter than {MIN_CLOCK_S * 1e3:.0f} ms"
     res[k] = e
 os.makedirs(out_dir, exist_ok=True)
 json.dump(res, open(os.path.join(out_dir, f"pmc_summary_{cfg}.json" if cfg else "pmc_summary.json"), "w"), indent=1)
