@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdarg>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -93,6 +95,19 @@ struct Launch {
 
 namespace {
 int hip_status(hipError_t e) { return e == hipSuccess ? BM_OK : BM_EHIP; }
+
+// BTCMINER_TRACE=1: one stderr line per step of the group set-up and combine
+// (diagnostics of multi-process runs; off by default)
+void trace(const char* fmt, ...) {
+    static const bool on = std::getenv("BTCMINER_TRACE") != nullptr;
+    if (!on) return;
+    va_list ap;
+    va_start(ap, fmt);
+    std::fprintf(stderr, "[btcminer] ");
+    std::vfprintf(stderr, fmt, ap);
+    std::fprintf(stderr, "\n");
+    va_end(ap);
+}
 
 #define BM_HIP(call)                                 \
     do {                                             \
@@ -944,11 +959,15 @@ int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
     cfg.blocking = 0;
     ncclComm_t comm = nullptr;
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+    bm::trace("rank %d/%d: ncclCommInitRankConfig (non-blocking, timeout %d ms)", ctx->rank, ctx->world, timeout_ms);
     ncclResult_t r = ncclCommInitRankConfig(&comm, ctx->world, u, ctx->rank, &cfg);
+    bm::trace("rank %d: init returned %d", ctx->rank, (int)r);
     int rc = (r == ncclSuccess || r == ncclInProgress) ? BM_OK : BM_ERCCL;
     if (rc == BM_OK && r == ncclInProgress) rc = bm::comm_settle(comm, r, deadline, timeout_ms > 0);
+    bm::trace("rank %d: join status %d", ctx->rank, rc);
     if (rc != BM_OK) {
         if (comm) (void)ncclCommAbort(comm);
+        bm::trace("rank %d: communicator aborted", ctx->rank);
         return rc;
     }
     d.comm = comm;
