@@ -16,6 +16,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -364,6 +367,54 @@ int comm_settle(ncclComm_t comm, ncclResult_t r, std::chrono::steady_clock::time
         if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) return BM_ERCCL;
     }
     return r == ncclSuccess ? BM_OK : BM_ERCCL;
+}
+
+// bm_ctx_join_rank's worker: one communicator set-up, shared with the caller
+// (who may give up on it: then the worker aborts what it made).
+struct JoinJob {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclComm_t comm = nullptr;
+    int rc = BM_ERCCL;
+};
+
+void join_worker(std::shared_ptr<JoinJob> job, int dev, int world, int rank, ncclUniqueId u) {
+    ncclComm_t comm = nullptr;
+    int rc = BM_ERCCL;
+    if (hipSetDevice(dev) == hipSuccess) {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclResult_t r = ncclCommInitRankConfig(&comm, world, u, rank, &cfg);
+        trace("rank %d: init returned %d", rank, (int)r);
+        while (r == ncclInProgress) {
+            {
+                std::lock_guard<std::mutex> g(job->m);
+                if (job->abandoned) break;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+            if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) r = ncclInternalError;
+        }
+        rc = r == ncclSuccess ? BM_OK : BM_ERCCL;
+    }
+    // publish; a communicator nobody will use (a failed set-up, or a caller
+    // that gave up) is aborted first, outside the lock: an abort may block,
+    // and the caller's timed wait must still be able to take the lock
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> g(job->m);
+            if (!comm || (rc == BM_OK && !job->abandoned)) {
+                job->comm = comm;
+                job->rc = rc;
+                job->done = true;
+                job->cv.notify_all();
+                return;
+            }
+        }
+        (void)ncclCommAbort(comm);
+        comm = nullptr;
+        trace("rank %d: communicator aborted", rank);
+    }
 }
 
 // Waits for everything a call may have queued on any stream of the context.
@@ -953,24 +1004,31 @@ int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
     if (hipSetDevice(d.id) != hipSuccess) return BM_EHIP;
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
-    // non-blocking, so a group that never forms (a peer that died before
-    // joining) costs timeout_ms, not a hang
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;
-    ncclComm_t comm = nullptr;
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
-    bm::trace("rank %d/%d: ncclCommInitRankConfig (non-blocking, timeout %d ms)", ctx->rank, ctx->world, timeout_ms);
-    ncclResult_t r = ncclCommInitRankConfig(&comm, ctx->world, u, ctx->rank, &cfg);
-    bm::trace("rank %d: init returned %d", ctx->rank, (int)r);
-    int rc = (r == ncclSuccess || r == ncclInProgress) ? BM_OK : BM_ERCCL;
-    if (rc == BM_OK && r == ncclInProgress) rc = bm::comm_settle(comm, r, deadline, timeout_ms > 0);
-    bm::trace("rank %d: join status %d", ctx->rank, rc);
-    if (rc != BM_OK) {
-        if (comm) (void)ncclCommAbort(comm);
-        bm::trace("rank %d: communicator aborted", ctx->rank);
-        return rc;
+    // The join runs on a worker thread: a non-blocking ncclCommInitRankConfig
+    // polled until it settles.  With a timeout the caller waits at most that
+    // long; past it the worker is left to abort the communicator in the
+    // background (neither the init of a group whose peer never comes nor
+    // its abort is guaranteed to return promptly), and the call returns
+    // BM_ETIMEDOUT.
+    auto job = std::make_shared<bm::JoinJob>();
+    const int dev = d.id, world = ctx->world, rank = ctx->rank;
+    bm::trace("rank %d/%d: joining (timeout %d ms)", rank, world, timeout_ms);
+    std::thread worker([job, dev, world, rank, u]() { bm::join_worker(job, dev, world, rank, u); });
+    std::unique_lock<std::mutex> lk(job->m);
+    if (timeout_ms == 0) {
+        job->cv.wait(lk, [&] { return job->done; });
+    } else if (!job->cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return job->done; })) {
+        job->abandoned = true;
+        lk.unlock();
+        worker.detach();
+        bm::trace("rank %d: join timed out; the communicator is aborted in the background", rank);
+        return BM_ETIMEDOUT;
     }
-    d.comm = comm;
+    lk.unlock();
+    worker.join();
+    bm::trace("rank %d: join status %d", rank, job->rc);
+    if (job->rc != BM_OK) return job->rc;
+    d.comm = job->comm;
     ctx->joined = true;
     ctx->group_status = BM_OK;
     return BM_OK;
