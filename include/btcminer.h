@@ -101,8 +101,10 @@ int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out);
  *   2. once every rank has created its context (exchange the statuses over
  *      the side channel), rank 0 calls bm_rccl_unique_id() and hands the
  *      bytes to every rank, and each calls bm_ctx_join_rank(): a
- *      non-blocking ncclCommInitRankConfig, polled for at most timeout_ms
- *      (0: no limit) and aborted after it.  From then on a search ends with
+ *      non-blocking ncclCommInitRankConfig on a worker thread; the call
+ *      waits for it at most timeout_ms (0: no limit) and then returns
+ *      BM_ETIMEDOUT, leaving the worker to abort the communicator (RCCL's
+ *      bootstrap can block until every rank has connected).  From then on a search ends with
  *      one RCCL allgather of 32-byte slots {hash, nonce, status, 0}, so
  *      every rank returns the whole range's answer -- or, when any rank
  *      failed the call before the combine (it still takes part, with its
