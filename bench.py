@@ -231,7 +231,7 @@ def hip_runtimes():
     return sorted({ln.split()[-1] for ln in maps if "libamdhip64" in ln})
 
 
-def cpu_baseline(target_s=10.0):
+def cpu_baseline(target_s=6.0):
     """Time the oracle loop (test infrastructure: the CPU 'port' of
     hash.go + miner.go) on this host over a bounded sample of C2."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
