@@ -17,18 +17,24 @@ Workloads (--config):
 
 How N GPUs are driven (--gpus N):
   * torchrun (WORLD_SIZE = N > 1, the driver's multi-GPU launch): one process
-    per GPU.  Each rank opens a library context that is one rank of an RCCL
-    group (bm_ctx_create_rank on LOCAL_RANK; rank 0's unique id travels over
-    the rendezvous), every rank calls bm_search_gpu on the WHOLE range, scans
-    its contiguous piece, and one RCCL allgather of the 16-byte partials gives
-    every rank the answer.  The unique id, the barriers and the max over
-    ranks go through a file rendezvous on the node
-    (distributed_bitcoin_minter_amd/rendezvous.py): no torch in any rank, so
-    each process maps one HIP runtime, /opt/rocm's, the one the GPU test
-    suite runs on, and only the ranks themselves hold the GPUs.
+    per GPU.  Each rank opens a rank context of the library on its device
+    (LOCAL_RANK, or the one device a per-rank visibility mask leaves it),
+    the ranks compare their status, and all of them join one RCCL group
+    (rank 0's unique id travels over the rendezvous; the join is bounded).
+    Every rank calls bm_search_gpu on the WHOLE range, scans its contiguous
+    piece, and one RCCL allgather of 32-byte slots (partial + status) gives
+    every rank the answer.  If any rank cannot join, every rank leaves and
+    the 16-byte partials of their contexts are gathered over the
+    rendezvous; config.parallelism says which combine ran and why.  The
+    unique id, the barriers and the max over ranks go through a file
+    rendezvous on the node (distributed_bitcoin_minter_amd/rendezvous.py):
+    no torch in any rank, so each process maps one HIP runtime, /opt/rocm's,
+    the one the GPU test suite runs on, and only the ranks themselves hold
+    the GPUs.
   * no launcher, N > 1: ONE process drives N devices (BASELINE C4's design):
     a multi-device context splits the range and combines with
-    ncclCommInitAll + ncclAllGather inside the library.  Fewer than N visible
+    ncclCommInitAll + ncclAllGather inside the library (host copies if RCCL
+    fails at run time, reported in the line).  Fewer than N visible
     devices is an error, unless --rehearse-one-gpu (every "device" is GPU 0,
     partials combined on the host: checks the N-way split, not a measurement).
   * N = 1: one device, no collective.
@@ -44,9 +50,13 @@ Also reported:
   roofline      the dominant launch: algorithmic int32 ops (nonces x C x 1384,
                 SURVEY.md §8d, C = SHA-256 blocks the kernel compresses per
                 nonce) / its HIP-event time on the library's stream, vs 78.64 T
-                lane-ops/s per GPU; PMC figures (VALU per nonce, clock under
-                the kernel, memory-side bytes) from profiles/<round>/ for the
-                same config.
+                lane-ops/s per GPU; the issue bound of the kernel's loop at
+                the clock measured on this box after the timed region
+                (measure_clock); PMC figures (VALU per nonce, memory-side
+                bytes) from profiles/<round>/ for the same config.
+  config.ranks / config.devices
+                each rank's (device's) nonces, GPU span and rate, and the
+                combine that ran.
   cpu_baseline  the oracle's loop shape (format + SHA-256 + strict '<') on this
                 host's cores over a bounded sample of C2 (rank 0, N = 1 only);
                 "system": one LSP server + N single-threaded CPU miner processes

@@ -630,7 +630,7 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
         (void)hipStreamSynchronize(d.stream);
         (void)hipGetLastError();
         st.rccl_status = rc;
-        return rc;
+        return own_rc != BM_OK ? own_rc : rc;  // this rank's own failure stays the one it reports
     }
     st.combine_used = BM_COMBINED_RCCL;
     for (int r = 0; r < world; ++r)
