@@ -207,7 +207,17 @@ def _bench(args, env=None, torchrun=0):
             port = s.getsockname()[1]
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={torchrun}",
                "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py")] + args
-    return subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    # its own process group: on a hang, torchrun's workers die with it
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=300)
+    except subprocess.TimeoutExpired:
+        import signal
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        pytest.fail(f"bench {args} did not finish in 300 s: {err[-2000:]}")
+    return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
 
 def _line(r):
@@ -270,11 +280,12 @@ from distributed_bitcoin_minter_amd import BtcMinerError, Context, rccl_unique_i
 from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
 with Rendezvous(timeout_s=120) as rz:
     uid = rz.broadcast_bytes(rccl_unique_id() if rz.rank == 0 else None)
-    try:
-        with Context(devices=[0], rank=rz.rank, world=rz.world, unique_id=uid) as c:
+    with Context(devices=[0], rank=rz.rank, world=rz.world) as c:
+        try:
+            c.join(uid, timeout_ms=60_000)  # bounded: a box where RCCL waits instead of refusing costs 60 s
             status = 0
-    except BtcMinerError as e:
-        status = e.status
+        except BtcMinerError as e:
+            status = e.status
     seen = rz.all_gather(status)
 print(json.dumps({"rank": rz.rank, "status": status, "seen": seen}))
 """
@@ -282,9 +293,9 @@ print(json.dumps({"rank": rz.rank, "status": status, "seen": seen}))
 
 def test_rank_group_bootstrap_two_ranks_one_gpu():
     """Two rank contexts on the SAME GPU: the unique id made by rank 0 reaches
-    rank 1 over the rendezvous, both join RCCL's bootstrap, and RCCL then
-    refuses the duplicate GPU -- both ranks get BM_ERCCL promptly (no hang),
-    which is what bench.py's fallback relies on.  (Two distinct GPUs would
+    rank 1 over the rendezvous, both join RCCL's bootstrap (bm_ctx_join_rank,
+    bounded), and RCCL then refuses the duplicate GPU -- both ranks get
+    BM_ERCCL promptly (no hang), which is what bench.py's fallback relies on.  (Two distinct GPUs would
     form the group: the driver's multi-GPU run.)"""
     import socket
     from distributed_bitcoin_minter_amd._lib import BM_ERCCL
@@ -298,10 +309,16 @@ def test_rank_group_bootstrap_two_ranks_one_gpu():
         procs.append(subprocess.Popen([sys.executable, "-c", _RANK_BOOT, ROOT], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []
-    for p in procs:
-        o, e = p.communicate(timeout=240)
-        assert p.returncode == 0, e[-3000:]
-        outs.append(json.loads(o.strip().splitlines()[-1]))
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=180)
+            assert p.returncode == 0, e[-3000:]
+            outs.append(json.loads(o.strip().splitlines()[-1]))
+    finally:
+        for p in procs:  # never leave a rank holding the GPU
+            if p.poll() is None:
+                p.kill()
+                p.wait()
     assert all(o["seen"] == [BM_ERCCL, BM_ERCCL] for o in outs), outs
 
 
