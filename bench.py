@@ -166,23 +166,33 @@ def issue_bound(p, nbv, clock_ghz):
 
 class ClockSampler:
     """The driver's gfx clock of one GPU (hwmon freq1_input, found through
-    the device's PCI bus id) sampled every `period` s on a host thread while
-    the timed region runs, with no change to the kernels.  It tracks the PMC
-    clock to about 1% (it reads high: 2.235-2.241 GHz against 2.20-2.22 by
-    PMC on one box, profiles/r02/s2_clock_sources.log), so it is reported
-    beside the issue bound, and per rank at N > 1, not used for it.  Silent
-    (None) where sysfs does not expose it."""
+    the device's PCI bus id), and its board power where hwmon has it
+    (power1_average or power1_input, against power1_cap), sampled every
+    `period` s on a host thread, with no change to the kernels.  Silent
+    (None) where sysfs does not expose them."""
 
     def __init__(self, device, period=0.05):
         import threading
-        self.period, self.samples, self.path = period, [], None
+        self.period, self.samples, self.watts, self.path, self.ppath, self.cap_w = period, [], [], None, None, None
         if period is None:  # off
             self._thread = None
             return
         try:
             bus = device_pci_bus_id(device).lower()
-            paths = sorted(glob.glob(f"/sys/bus/pci/devices/{bus}/hwmon/hwmon*/freq1_input"))
-            self.path = paths[0] if paths else None
+            hw = sorted(glob.glob(f"/sys/bus/pci/devices/{bus}/hwmon/hwmon*"))
+            for h in hw:
+                if os.path.exists(os.path.join(h, "freq1_input")):
+                    self.path = os.path.join(h, "freq1_input")
+                    for name in ("power1_average", "power1_input"):
+                        if os.path.exists(os.path.join(h, name)):
+                            self.ppath = os.path.join(h, name)
+                            break
+                    try:
+                        with open(os.path.join(h, "power1_cap")) as f:
+                            self.cap_w = int(f.read()) / 1e6
+                    except (OSError, ValueError):
+                        self.cap_w = None
+                    break
         except Exception:  # noqa: BLE001 -- informational only
             self.path = None
         self._stop = threading.Event()
@@ -193,6 +203,9 @@ class ClockSampler:
             try:
                 with open(self.path) as f:
                     self.samples.append(int(f.read()))
+                if self.ppath:
+                    with open(self.ppath) as f:
+                        self.watts.append(int(f.read()) / 1e6)
             except (OSError, ValueError):
                 return
             self._stop.wait(self.period)
@@ -209,13 +222,18 @@ class ClockSampler:
         self._thread.join()
         return sum(self.samples) / len(self.samples) / 1e9 if self.samples else None
 
+    def power(self):
+        """(mean board power in W, its cap in W), either None where absent."""
+        return (sum(self.watts) / len(self.watts) if self.watts else None), self.cap_w
+
 
 def measure_clock(dev, msg, digits, lo, hi, seconds=0.5, max_nonces=1 << 32):
     """The driver's gfx clock of GPU `dev` while the dominant kernel runs:
     hwmon freq1_input sampled every 10 ms over untimed searches of that
     kernel's digit range (at most 2^32 nonces of it) on a context of its own,
-    so the step's smaller launches (which clock higher) do not bias it.
-    Returns {ghz, lower, upper, searches} or None where sysfs has no clock."""
+    so the step's smaller launches (which clock higher) do not bias it; the
+    board power over the same searches where hwmon has it.  Returns {ghz,
+    lower, upper, searches, watts, cap_w} or None where sysfs has no clock."""
     a = max(lo, 10 ** (digits - 1))
     b = min(hi, 10 ** digits - 1, a + max_nonces - 1)
     if a > b:
@@ -229,7 +247,8 @@ def measure_clock(dev, msg, digits, lo, hi, seconds=0.5, max_nonces=1 << 32):
             c.search(msg, a, b)
             k += 1
         ghz = smp.stop()
-    return {"ghz": ghz, "lower": a, "upper": b, "searches": k} if ghz else None
+    watts, cap = smp.power()
+    return {"ghz": ghz, "lower": a, "upper": b, "searches": k, "watts": watts, "cap_w": cap} if ghz else None
 
 
 def hip_runtimes():
@@ -639,6 +658,12 @@ def main():
         box = box_clock or {}
         if box.get("ghz"):
             roof["clock_ghz_box"] = round(box["ghz"], 3)
+        if box.get("watts"):
+            # board power while the dominant kernel ran, against its cap: the
+            # clock this kernel gets is set by power
+            roof["power_w_box"] = round(box["watts"], 1)
+            if box.get("cap_w"):
+                roof["power_cap_w"] = round(box["cap_w"], 1)
         ib_clock = live_clock or box.get("ghz")
         ib = issue_bound(dom.p, dom.nbv, ib_clock or clock or 0.0) if (ib_clock or clock) else None
         if ib:
