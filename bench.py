@@ -145,6 +145,14 @@ def pmc_summary(config, p, nbv=1):
     return None, None
 
 
+def kernel_compressions(L):
+    """SHA-256 compressions one launch does per nonce: the varying block,
+    plus the constant padding block when the length does not fit (P >= 55);
+    an NBV = 2 launch re-compresses the block before once per task of
+    10^inner_digits nonces, not once per nonce (tools/len_sweep.py)."""
+    return 1 + L.pad_block + (L.nbv - 1) / 10 ** L.inner_digits
+
+
 def issue_bound(p, nbv, clock_ghz):
     """gfx950 VALU issue bound of the kernel's inner loop: each
     slow op (v_alignbit, v_add3, SGPR operand, ...) takes an issue slot of its
@@ -529,7 +537,7 @@ def main():
         dom = max(launches, key=lambda L: L.nonces, default=None)
         # this device's algorithmic ops over the call's GPU span (first
         # launch start to last launch end): launches overlap on two streams
-        ops = sum(L.nonces * (L.nbv + L.pad_block) for L in launches) * OPS_PER_COMPRESSION
+        ops = sum(L.nonces * kernel_compressions(L) for L in launches) * OPS_PER_COMPRESSION
         per = {"nonces": st.nonces, "span_ms": st.span_ms, "combine": COMBINED_NAMES.get(st.combine_used, "?"),
                "rccl_status": st.rccl_status,
                "devices": [(st.dev_nonces[i], st.dev_span_ms[i]) for i in range(st.devices)]}
@@ -611,7 +619,7 @@ def main():
     if dom is not None:
         ms = [d[0].ms for d in doms if d[0] is not None]
         dom_ms = sum(ms) / len(ms)
-        c_eff = dom.nbv + dom.pad_block  # blocks the kernel compresses per nonce
+        c_eff = kernel_compressions(dom)  # blocks the kernel compresses per nonce
         c_survey = compressions_per_nonce(len(msg), dom.digits)
         achieved = dom.nonces * c_eff * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
         pmc, pmc_src = pmc_summary(args.config, dom.p, dom.nbv)

@@ -179,3 +179,15 @@ def test_bench_ranks_stop_together_when_one_context_fails():
     outs = _rank_setup(3, FAKE_FAIL="create:2")
     assert [rc for rc, _, _ in outs] == [1, 1, 1], outs
     assert all("rank 2" in e for _, _, e in outs)
+
+
+def test_kernel_compressions_per_nonce():
+    """The roofline counts the blocks a launch really compresses per nonce:
+    1 for the plain layouts, 2 with the constant padding block, and for an
+    NBV = 2 launch 1 + 1/task (the block before is re-compressed once per
+    task of 10^inner_digits nonces)."""
+    from types import SimpleNamespace as L
+    assert bench.kernel_compressions(L(nbv=1, pad_block=0, inner_digits=2)) == 1
+    assert bench.kernel_compressions(L(nbv=1, pad_block=1, inner_digits=2)) == 2
+    assert bench.kernel_compressions(L(nbv=2, pad_block=0, inner_digits=2)) == 1.01
+    assert bench.kernel_compressions(L(nbv=2, pad_block=0, inner_digits=1)) == 1.1

@@ -7,7 +7,8 @@ reaches, timed on the GPU.
 For each message length L in 0..max_len (bytes 'a'..), one search of
 [10^9, 10^9 + nonces - 1] (all 10-digit, so one layout per L: P, NBV, padding
 block) after a warm-up call; prints one JSON line per L with GH/s and the
-compressions the kernel does per nonce (NBV + padding block), so layouts can
+compressions the kernel does per nonce (1, + the padding block, + 1/task for
+NBV = 2), so layouts can
 be compared per compression: G compressions/s should sit near the C2 figure
 for every layout.  The answers are not checked here (tests/test_gpu_parity.py
 checks every layout); this is a measurement."""
@@ -35,9 +36,9 @@ def main():
                 st = ctx.last_stats()
                 if best is None or st.wall_ms < best[0]:
                     dom = max((st.launch[i] for i in range(st.recorded)), key=lambda x: x.nonces)
-                    best = (st.wall_ms, dom.p, dom.nbv, dom.pad_block, dom.nonces, dom.ms, st.launches)
-            wall, p, nbv, pad, dn, dms, nl = best
-            c = nbv + pad
+                    best = (st.wall_ms, dom.p, dom.nbv, dom.pad_block, dom.nonces, dom.ms, st.launches, dom.inner_digits)
+            wall, p, nbv, pad, dn, dms, nl, ms = best
+            c = 1 + pad + (nbv - 1) / 10 ** ms  # NBV = 2: the block before once per task
             print(json.dumps({"len": L, "P": p, "nbv": nbv, "pad": pad, "launches": nl,
                               "GHs": round(n / wall / 1e6, 3), "Gcomp_s": round(c * n / wall / 1e6, 3),
                               "dom_GHs": round(dn / dms / 1e6, 3) if dms > 0 else None}), flush=True)
