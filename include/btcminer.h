@@ -75,7 +75,8 @@ int bm_device_pci_bus_id(int device, char* buf, int len);
 
 /* Context over devices 0..num_gpus-1 (num_gpus = 0: all visible devices).
  * A context with several devices splits every search across them and
- * combines the per-device 16-byte partials with one RCCL allgather.
+ * combines the per-device partials with one RCCL allgather (host copies if
+ * RCCL fails at run time; see bm_ctx_set_combine).
  * Launch-overlap tuning is read from the environment at creation (results
  * never depend on it): BTCMINER_STREAMS = launch streams per device (1..4,
  * default 2); BTCMINER_TAIL = nonces split off the biggest launch into a
