@@ -28,6 +28,10 @@ of the same kernels, and the build fails on any violation:
    --cluster) can shorten a pair the compiler padded (VALU writes VGPR ->
    DPP / v_readlane / v_readfirstlane, VALU writes SGPR -> VMEM / lane
    select, store data -> overwrite) and is refused there.
+4. New pairs.  An inserted instruction that reads or writes registers may
+   not form, with any instruction within 6 issue slots of it, a pair the
+   hardware does not interlock (conservatively: an SALU write feeding a
+   VMEM address counts as one).
 
 bm_prio marks what it produced with `Made` lines: unchanged lines pass
 through as the same Python objects, so the guard pairs each line of the
@@ -339,6 +343,34 @@ def check(orig, final, kernels):
             if ln.kind != "rewrite" and hit:
                 problems.append(f"{short}: `{ln.strip()}` (line {i - flo}) touches {sorted(hit)} while a load "
                                 f"into it is outstanding")
+        # 4: an inserted instruction against its neighbours: as a new producer
+        # or consumer of a register it must not form a pair the hardware does
+        # not interlock within the window (e.g. an SGPR written just before a
+        # VMEM reads it, or a VGPR written just after a store issued with it)
+        seq, slot = [], 0
+        for i in range(flo, fhi):
+            if is_insn(final[i]):
+                seq.append((i, insns[i], slot))
+                slot += insns[i].slots
+        for k, (i, x, sx) in enumerate(seq):
+            if not (isinstance(final[i], Made) and final[i].kind == "insert") or not (x.reads | x.writes):
+                continue
+            for j in range(k - 1, -1, -1):
+                _i, y, sy = seq[j]
+                if sx - sy >= WINDOW:
+                    break
+                bad = [r for r in y.writes & (x.reads | x.writes) if not _interlocked(y, x, r)]
+                if y.reads & x.writes and (y.mem == "vm" or y.mn.startswith(("ds_", "v_readlane", "v_readfirstlane"))):
+                    bad += sorted(y.reads & x.writes)
+                if bad:
+                    problems.append(f"{short}: inserted `{final[i].strip()}` after `{y.line.strip()}` on {sorted(set(bad))}")
+            for j in range(k + 1, len(seq)):
+                _i, z, sz = seq[j]
+                if sz - sx >= WINDOW:
+                    break
+                bad = [r for r in x.writes & (z.reads | z.writes) if not _interlocked(x, z, r)]
+                if bad:
+                    problems.append(f"{short}: inserted `{final[i].strip()}` before `{z.line.strip()}` on {sorted(set(bad))}")
         # 3: wait states between the compiler's instructions
         olo, ohi = o_k[name]
         oins = [(id(orig[i]), Insn(orig[i])) for i in range(olo, ohi) if is_insn(orig[i])]

@@ -385,6 +385,12 @@ _ZN2bm13search_kernelILi16ELi1EEEvNS_10SearchArgsEPNS_7PartialEPy:
 \ts_waitcnt lgkmcnt(0)
 \tv_mov_b32_e32 v4, s0
 \tv_add_u32_e32 v5, v4, v2
+\tv_xor_b32_e32 v6, v5, v4
+\tv_xor_b32_e32 v7, v6, v4
+\tv_xor_b32_e32 v8, v7, v4
+\tv_xor_b32_e32 v9, v8, v4
+\tv_xor_b32_e32 v10, v9, v4
+\tv_xor_b32_e32 v11, v10, v4
 \tglobal_store_dwordx4 v12, v[0:3], s[0:1]
 \ts_endpgm
 .Lfunc_end5:
@@ -404,10 +410,16 @@ def test_guard_refuses_a_write_racing_an_outstanding_smem_load():
     with pytest.raises(guard.GuardError, match=r"s_mov_b32 s0, s0.*\['s0'\].*outstanding"):
         guard.check(orig, bad, ["search_kernel"])
     guard.check(orig, _passes(orig, spacer="\ts_nop 0\n"), ["search_kernel"])
-    # the same instruction inserted after the wait is fine
+    # the same instruction inserted after the wait, away from any memory op, is fine ...
     late = list(orig)
     late.insert(6, guard.Made("\ts_mov_b32 s0, s0\n", "insert"))
     guard.check(orig, late, ["search_kernel"])
+    # ... but not right before the store that reads s[0:1] as its address
+    # (rule 4, conservative: an SALU write feeding a VMEM address)
+    near = list(orig)
+    near.insert(14, guard.Made("\ts_mov_b32 s0, s0\n", "insert"))
+    with pytest.raises(guard.GuardError, match="before `global_store_dwordx4"):
+        guard.check(orig, near, ["search_kernel"])
 
 
 def test_guard_counter_model():
