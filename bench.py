@@ -236,27 +236,41 @@ class ClockSampler:
 
 
 def measure_clock(dev, msg, digits, lo, hi, seconds=0.5, max_nonces=1 << 32):
-    """The driver's gfx clock of GPU `dev` while the dominant kernel runs:
-    hwmon freq1_input sampled every 10 ms over untimed searches of that
-    kernel's digit range (at most 2^32 nonces of it) on a context of its own,
-    so the step's smaller launches (which clock higher) do not bias it; the
-    board power over the same searches where hwmon has it.  Returns {ghz,
-    lower, upper, searches, watts, cap_w} or None where sysfs has no clock."""
+    """The clock of GPU `dev` while the dominant kernel runs, measured after
+    the timed region on a context of its own, over untimed searches of that
+    kernel's digit range (at most 2^32 nonces of it), so the step's smaller
+    launches (which clock higher) do not bias it:
+      * live: the same kernels built with the clock probe
+        (libbtcminer_probe.so, `make -C csrc probe`) stamp s_memtime (shader
+        cycles) and s_memrealtime (100 MHz) at the start and end of each
+        launch: the dominant launch's own average clock;
+      * sysfs: the driver's gfx clock (hwmon freq1_input) and board power
+        sampled every 10 ms over the same searches.
+    Returns {ghz_live, ghz, watts, cap_w, lower, upper, searches} or None."""
     a = max(lo, 10 ** (digits - 1))
     b = min(hi, 10 ** digits - 1, a + max_nonces - 1)
     if a > b:
         return None
-    with Context(devices=[dev]) as c:
+    probe = _lib.PROBE_LIB_PATH if os.path.exists(_lib.PROBE_LIB_PATH) else None
+    live = []
+    with Context(devices=[dev], lib_path=probe) as c:
+        c.set_timing(True)
         c.search(msg, a, b)
         smp = ClockSampler(dev, period=0.01)
         smp.start()
         t, k = time.perf_counter(), 0
         while k < 3 or time.perf_counter() - t < seconds:
             c.search(msg, a, b)
+            st = c.last_stats()
+            dom = max((st.launch[i] for i in range(st.recorded)), key=lambda L: L.nonces, default=None)
+            if dom is not None and dom.clock_ghz > 0:
+                live.append(dom.clock_ghz)
             k += 1
         ghz = smp.stop()
     watts, cap = smp.power()
-    return {"ghz": ghz, "lower": a, "upper": b, "searches": k, "watts": watts, "cap_w": cap} if ghz else None
+    out = {"ghz_live": sum(live) / len(live) if live else None, "ghz": ghz, "watts": watts, "cap_w": cap,
+           "lower": a, "upper": b, "searches": k}
+    return out if (out["ghz_live"] or ghz) else None
 
 
 def hip_runtimes():
@@ -664,6 +678,8 @@ def main():
             # the driver's gfx clock over the whole timed steps (every launch)
             roof["clock_ghz_sysfs"] = round(sysfs_clock, 3)
         box = box_clock or {}
+        if box.get("ghz_live"):
+            roof["clock_ghz_box_live"] = round(box["ghz_live"], 3)
         if box.get("ghz"):
             roof["clock_ghz_box"] = round(box["ghz"], 3)
         if box.get("watts"):
@@ -672,13 +688,15 @@ def main():
             roof["power_w_box"] = round(box["watts"], 1)
             if box.get("cap_w"):
                 roof["power_cap_w"] = round(box["cap_w"], 1)
-        ib_clock = live_clock or box.get("ghz")
+        ib_clock = live_clock or box.get("ghz_live") or box.get("ghz")
         ib = issue_bound(dom.p, dom.nbv, ib_clock or clock or 0.0) if (ib_clock or clock) else None
         if ib:
             if ib_clock:
-                ib["clock_src"] = ("live (s_memtime / s_memrealtime)" if live_clock else
-                                   f"this box: hwmon freq1_input every 10 ms over {box['searches']} untimed "
-                                   f"searches of the dominant kernel's range [{box['lower']}, {box['upper']}]")
+                where = (f"{box.get('searches')} untimed searches of the dominant kernel's range "
+                         f"[{box.get('lower')}, {box.get('upper')}] on this box")
+                ib["clock_src"] = ("live (s_memtime / s_memrealtime) in the timed launches" if live_clock else
+                                   f"live (s_memtime / s_memrealtime, libbtcminer_probe.so) over {where}"
+                                   if box.get("ghz_live") else f"hwmon freq1_input every 10 ms over {where}")
                 ib["frac"] = round(dom.nonces / (dom_ms * 1e-3) / 1e9 / ib["GHs_per_gpu"], 4)
             else:
                 ib["clock_src"] = pmc_src

@@ -67,21 +67,38 @@ class BtcMinerError(RuntimeError):
 
 
 _lib = None
+_variants = {}
+# The same library built with BM_CLOCK_PROBE=1 (`make -C csrc probe`): its
+# launches stamp the shader clock.  bench.py loads it beside the product
+# library, only to measure the clock under the dominant kernel after the
+# timed region; nothing else uses it.
+PROBE_LIB_PATH = os.path.join(_HERE, "libbtcminer_probe.so")
 
 
-def load():
-    """Load libbtcminer.so once; raises OSError if it has not been built."""
+def load(path=None):
+    """Load libbtcminer.so once (or, with a path, another build of the same
+    ABI, e.g. PROBE_LIB_PATH); raises OSError if it has not been built."""
     global _lib
+    if path is not None and os.path.abspath(path) != os.path.abspath(LIB_PATH):
+        path = os.path.abspath(path)
+        if path not in _variants:
+            _variants[path] = _open(path)
+        return _variants[path]
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise OSError(f"{LIB_PATH} is missing: build it with `make -C {os.path.join(_HERE, 'csrc')} -j8` "
+    _lib = _open(LIB_PATH)
+    return _lib
+
+
+def _open(path):
+    if not os.path.exists(path):
+        raise OSError(f"{path} is missing: build it with `make -C {os.path.join(_HERE, 'csrc')} -j8` "
                       "(or __graft_entry__.build())")
     # RTLD_NOW: every HIP/RCCL symbol of the library (and of the runtime it
     # pulls in) binds at load time.  A process that imports torch afterwards
     # maps torch's bundled HIP runtime too; lazy binding could then resolve
     # some of our calls into that second runtime.
-    lib = ctypes.CDLL(LIB_PATH, mode=os.RTLD_NOW | os.RTLD_LOCAL)
+    lib = ctypes.CDLL(path, mode=os.RTLD_NOW | os.RTLD_LOCAL)
     P = ctypes.POINTER
     vp = ctypes.c_void_p
     sigs = {
@@ -129,8 +146,7 @@ def load():
     # the stats structs above are this ABI's layout: any other build (an
     # older BTCMINER_LIB variant included) would be misread, so it is refused
     if lib.bm_abi_version() != BM_ABI_VERSION:
-        raise OSError(f"{LIB_PATH}: ABI version {lib.bm_abi_version()}, expected {BM_ABI_VERSION}; rebuild it")
-    _lib = lib
+        raise OSError(f"{path}: ABI version {lib.bm_abi_version()}, expected {BM_ABI_VERSION}; rebuild it")
     return lib
 
 
@@ -200,8 +216,8 @@ class Context:
     Context(devices=[d], rank=r, world=w, unique_id=uid): both steps at once
     (blocks until all w ranks join)."""
 
-    def __init__(self, devices=None, num_gpus=0, rank=None, world=None, unique_id=None):
-        lib = load()
+    def __init__(self, devices=None, num_gpus=0, rank=None, world=None, unique_id=None, lib_path=None):
+        lib = load(lib_path)
         h = ctypes.c_void_p()
         if world is not None:
             if devices is None or len(devices) != 1 or rank is None:

@@ -115,7 +115,7 @@ def test_library_loads_with_immediate_binding():
     /opt/rocm's runtime at load, before any later `import torch` maps torch's
     bundled copy (bench.py's torchrun path)."""
     import inspect
-    assert "RTLD_NOW" in inspect.getsource(_lib.load)
+    assert "RTLD_NOW" in inspect.getsource(_lib._open)
 
 
 def _c_client():

@@ -534,3 +534,19 @@ def test_bench_torchrun_with_per_rank_visibility_mask():
     ranks = sorted(cfg["ranks"], key=lambda r: r["rank"])
     assert [r["device"] for r in ranks] == [0, 0] and all(r["combine"] == "local" for r in ranks)
     assert sum(r["nonces"] for r in ranks) == cfg["global_nonces"]
+
+
+def test_clock_probe_library():
+    """libbtcminer_probe.so (the same kernels with BM_CLOCK_PROBE=1, which
+    bench.py loads beside the product library to measure the clock under the
+    dominant kernel) answers C2 like the product and reports a plausible live
+    shader clock for its launches."""
+    from distributed_bitcoin_minter_amd import _lib
+    if not os.path.exists(_lib.PROBE_LIB_PATH):
+        pytest.skip("libbtcminer_probe.so not built (make -C distributed_bitcoin_minter_amd/csrc probe)")
+    with Context(devices=[0], lib_path=_lib.PROBE_LIB_PATH) as c:
+        c.set_timing(True)
+        assert c.search(bytes.fromhex(C2["msg_hex"]), C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
+        st = c.last_stats()
+        dom = max((st.launch[i] for i in range(st.recorded)), key=lambda L: L.nonces)
+        assert 1.0 < dom.clock_ghz < 3.0, dom.clock_ghz
