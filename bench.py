@@ -512,8 +512,8 @@ def open_contexts(args, world, rank, local):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4"])
     ap.add_argument("--combine", default="rccl", choices=["rccl", "gather"],
                     help="torchrun ranks: in-library RCCL allgather (default) or a gather over the rendezvous")
