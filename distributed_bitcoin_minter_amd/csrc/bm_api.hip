@@ -1039,12 +1039,12 @@ int bm_ctx_leave_rank(bm_ctx_t* ctx) {
     bm::DeviceGuard guard;
     bm::DeviceCtx& d = ctx->devs[0];
     if (d.comm) {
+        // leaving is what a rank does when the group cannot be trusted (a
+        // peer failed to join, or the caller falls back): abort, which frees
+        // this rank's side without waiting for any peer
         (void)hipSetDevice(d.id);
         (void)hipStreamSynchronize(d.stream);
-        if (ctx->group_status == BM_OK)
-            (void)ncclCommDestroy(d.comm);
-        else
-            (void)ncclCommAbort(d.comm);
+        (void)ncclCommAbort(d.comm);
         d.comm = nullptr;
     }
     ctx->joined = false;
