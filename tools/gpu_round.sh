@@ -17,7 +17,7 @@
 #   c5          C5 at size: the native (C++) system and the Python one
 #   prof        rocprofv3 kernel traces of C2 (2 streams, 1 stream) and C3
 #   pmc         PMC passes (FETCH_SIZE, WRITE_SIZE, SQ) for C2 and C3, one counter group per run
-#   parity      tools/parity_campaign.py, 3,000 random cases
+#   parity      tools/parity_campaign.py, PARITY_CASES (3,000) random cases, seed PARITY_SEED (303)
 #   lensweep    tools/len_sweep.py: GH/s for every message length 0..130 (every layout a 10-digit search hits)
 #   ab          A/B of library variants: AB_LIBS="a.so b.so" (parity of each first, then alternating)
 # Logs and profiles land in gpurun_out/$TAG (TAG defaults to r03).
@@ -76,7 +76,7 @@ for phase in "$@"; do
           SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE -d "$OUT/pmc_${C}_sq" -o s --output-format csv \
           -- python3 tools/prof_one.py $C 2
       done ;;
-    parity) step parity_campaign 600 python -u tools/parity_campaign.py 3000 303 ;;
+    parity) step parity_campaign 600 python -u tools/parity_campaign.py ${PARITY_CASES:-3000} ${PARITY_SEED:-303} ;;
     lensweep) step len_sweep 600 python -u tools/len_sweep.py 130 ;;
     ab)
       for lib in $AB_LIBS; do
