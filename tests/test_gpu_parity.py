@@ -225,3 +225,23 @@ def test_tail_launch_split(oracle, monkeypatch, tail):
         for msg, lo, hi in ((b"bradfitz", 0, 3_000_000), (M120, 2**64 - 2_000_000, 2**64 - 1)):
             assert c.search(msg, lo, hi) == oracle.search(msg, lo, hi, threads=8)
         assert c.search(bytes.fromhex(c2["msg_hex"]), c2["lower"], c2["upper"]) == (c2["hash"], c2["nonce"])
+
+
+def test_maximum_message_sizes(gpu_ctx, oracle):
+    """Messages up to the ABI's maximum (BM_MAX_MSG_LEN = 1 MiB: README:61's
+    LSP payloads are ~1 KB, so this is far past anything a Request carries):
+    the host folds every whole block into the midstate and the kernel sees
+    only the tail, whatever the length; one byte more is refused."""
+    from distributed_bitcoin_minter_amd import BtcMinerError
+    from distributed_bitcoin_minter_amd._lib import BM_EINVAL
+    rng = random.Random(0x1EE7)
+    big = bytes(rng.randrange(256) for _ in range(1 << 20))
+    for L in (65_535, 65_536 + 55, (1 << 20) - 9, 1 << 20):
+        msg = big[:L]
+        lo = rng.randrange(10 ** 11, 10 ** 12)
+        assert gpu_ctx.search(msg, lo, lo + 99) == oracle.search(msg, lo, lo + 99, threads=8), L
+        ns = [rng.randrange(1 << 64) for _ in range(8)]
+        assert gpu_ctx.hash_many(msg, ns) == [oracle.hash(msg, n) for n in ns], L
+    with pytest.raises(BtcMinerError) as ei:
+        gpu_ctx.search(big + b"x", 0, 9)
+    assert ei.value.status == BM_EINVAL
