@@ -16,6 +16,7 @@
 #               per-rank visibility mask, C4 over 8 one-process slots
 #   c5          C5 at size: the native (C++) system and the Python one
 #   prof        rocprofv3 kernel traces of C2 (2 streams, 1 stream) and C3
+#   prof_driver rocprofv3 kernel trace of the driver's exact bench command
 #   pmc         PMC passes (FETCH_SIZE, WRITE_SIZE, SQ) for C2 and C3, one counter group per run
 #   parity      tools/parity_campaign.py, PARITY_CASES (3,000) random cases, seed PARITY_SEED (303)
 #   lensweep    tools/len_sweep.py: GH/s for every message length 0..130 (every layout a 10-digit search hits)
@@ -66,6 +67,11 @@ for phase in "$@"; do
         --output-format csv -- $BENCH --steps 5 --warmup 2
       step prof_C3 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_C3" -o run --output-format csv -- $BENCH --config C3 \
         --steps 5 --warmup 2 ;;
+    prof_driver)
+      # the driver's exact bench command under the kernel trace: the line's
+      # roofline.kernel_ms and rocprof's average for that kernel, same run
+      step prof_driver 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_driver" -o run --output-format csv \
+        -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     pmc)
       for C in C2 C3; do
         step pmc_${C}_fetch 90 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_${C}_fetch" -o f --output-format csv \
