@@ -512,8 +512,10 @@ def open_contexts(args, world, rank, local):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 40 at C2/C3, about 3 s of GPU time, so a coarse GPU-busy "
+                         "sampler sees the card busy; 2 at C4, 20 s each)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 5; 1 at C4)")
     ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4"])
     ap.add_argument("--combine", default="rccl", choices=["rccl", "gather"],
                     help="torchrun ranks: in-library RCCL allgather (default) or a gather over the rendezvous")
@@ -528,6 +530,10 @@ def main():
                     help="N-way split on ONE GPU (all ranks / devices are GPU 0): exercises the multi-GPU "
                          "path on a one-GPU box; not a scaling measurement")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 2 if args.config == "C4" else 40
+    if args.warmup is None:
+        args.warmup = 1 if args.config == "C4" else 5
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
