@@ -524,6 +524,10 @@ def main():
                     help="1: sample the driver's gfx clock during the timed region (reported, not used); "
                          "default: only at N > 1, where each rank's clock explains the scaling "
                          "(it cost about 0.1%% at N = 1, profiles/r02/s2_sampler_ab.log)")
+    ap.add_argument("--clock-seconds", type=float, default=4.0,
+                    help="length of the untimed clock measurement after the timed region (measure_clock); "
+                         "4 s also keeps the card busy long enough for a coarse GPU-busy sampler to see it, "
+                         "whatever --steps the caller passes")
     ap.add_argument("--no-balance", action="store_true",
                     help="keep near-equal pieces (default: after the warmup, pieces follow each GPU's measured rate)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -584,7 +588,7 @@ def main():
     # the clock under the dominant kernel on THIS box, for the issue bound
     # (untimed, after the timed region; every rank on its own GPU)
     dom0 = doms[-1][0]
-    box_clock = measure_clock(dev, msg, dom0.digits, lo, hi) if dom0 is not None else None
+    box_clock = measure_clock(dev, msg, dom0.digits, lo, hi, seconds=args.clock_seconds) if dom0 is not None else None
     grp.barrier()
 
     total = hi - lo + 1
