@@ -245,3 +245,35 @@ def test_maximum_message_sizes(gpu_ctx, oracle):
     with pytest.raises(BtcMinerError) as ei:
         gpu_ctx.search(big + b"x", 0, 9)
     assert ei.value.status == BM_EINVAL
+
+
+def test_failed_calls_leave_outputs_untouched(gpu_ctx):
+    """include/btcminer.h: "On failure the output arguments are left
+    untouched" -- a Go caller that ignores the status must not read a half
+    result.  Refused arguments (BM_EINVAL) and a search that fails part-way
+    (bm_ctx_set_test_fault: BM_EINTERNAL after some launches) leave a
+    sentinel result and hash array as they were; the context then answers
+    correctly again."""
+    import ctypes
+    from distributed_bitcoin_minter_amd import _lib
+    lib, h = _lib.load(), gpu_ctx.handle
+    sentinel = (0x0123456789ABCDEF, 0xFEDCBA9876543210)
+    r = _lib.Result(*sentinel)
+    big = b"\0" * ((1 << 20) + 1)
+    assert lib.bm_search_gpu(h, big, len(big), 0, 9, ctypes.byref(r)) == _lib.BM_EINVAL
+    assert lib.bm_search_gpu(h, None, 3, 0, 9, ctypes.byref(r)) == _lib.BM_EINVAL
+    assert (r.hash, r.nonce) == sentinel
+    try:
+        for k in (0, 1, 3):
+            gpu_ctx.set_test_fault(k)
+            assert lib.bm_search_gpu(h, b"bradfitz", 8, 0, (1 << 32) - 1, ctypes.byref(r)) == _lib.BM_EINTERNAL
+            assert (r.hash, r.nonce) == sentinel, k
+    finally:
+        gpu_ctx.set_test_fault(-1)  # the session's shared context
+    outs = (ctypes.c_uint64 * 4)(*([0xA5A5A5A5A5A5A5A5] * 4))
+    nonces = (ctypes.c_uint64 * 4)(0, 1, 2, 3)
+    assert lib.bm_hash_gpu(h, big, len(big), nonces, 4, outs) == _lib.BM_EINVAL
+    assert lib.bm_hash_gpu(h, b"msg", 3, None, 4, outs) == _lib.BM_EINVAL
+    assert list(outs) == [0xA5A5A5A5A5A5A5A5] * 4
+    assert lib.bm_search_gpu(h, b"msg", 3, 0, 2, ctypes.byref(r)) == _lib.BM_OK
+    assert (r.hash, r.nonce) == (4754799531757243342, 1)  # README:331
