@@ -132,3 +132,23 @@ def test_plan_c3_single_window():
     assert len(segs) == 1
     s = segs[0]
     assert (s.nbv, s.p, s.pad_block, s.digits, s.nd) == (1, 12, 0, 20, 13)
+
+
+try:
+    from hypothesis import HealthCheck, given, settings, strategies as st
+except ImportError:  # pragma: no cover - hypothesis is in the image
+    given = None
+
+if given is not None:
+    @settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+    @given(msg=st.binary(min_size=0, max_size=200),
+           lo=st.one_of(st.integers(0, 10 ** 6), st.integers(0, U64),
+                        st.sampled_from([10 ** k - 3 for k in range(1, 20)])),
+           width=st.one_of(st.integers(0, 50), st.integers(0, 10 ** 12), st.integers(0, U64)))
+    def test_plan_property_random_bytes_and_ranges(msg, lo, width):
+        """Any raw-byte message (Go's %s carries bytes unchanged) and any
+        inclusive range, clipped at 2^64-1: the segments tile the range in
+        ascending order, keep the kernel's compile-time words, and replay to
+        hashlib's SHA-256 of "msg nonce" at sampled nonces."""
+        hi = min(U64, lo + width)
+        check_plan(msg, lo, hi, random.Random(len(msg) ^ lo), samples=2)
