@@ -44,9 +44,11 @@ def Hash(msg, nonce: int) -> int:
 def go_json_string(s: str) -> str:
     """encoding/json's string encoder with HTML escaping (json.Marshal's
     default): <, >, & and control characters as \\u00XX (\\n, \\r, \\t short
-    forms), U+2028/U+2029 escaped, everything else raw UTF-8.  Lone
-    surrogates (what invalid UTF-8 decodes to here) become U+FFFD, as Go
-    replaces invalid UTF-8."""
+    forms), U+2028/U+2029 escaped, everything else raw UTF-8.  A lone
+    surrogate (what an invalid UTF-8 byte decodes to here, surrogateescape)
+    becomes the six characters \ufffd, which is what Go writes for each
+    invalid byte (encode.go: utf8.RuneError of width 1); a valid U+FFFD in
+    the string stays raw, as in Go."""
     out = ['"']
     for ch in s:
         o = ord(ch)
@@ -61,7 +63,7 @@ def go_json_string(s: str) -> str:
         elif o < 0x20 or ch in "<>&" or o in (0x2028, 0x2029):
             out.append("\\u%04x" % o)
         elif 0xD800 <= o <= 0xDFFF:
-            out.append("\ufffd")
+            out.append("\\ufffd")
         else:
             out.append(ch)
     out.append('"')

@@ -96,6 +96,26 @@ def test_client_wire_bytes_match_python():
         peer.close()
 
 
+@pytest.mark.parametrize("raw", [b"caf\xe9", b"a\xe2\x82b", b"\xed\xa0\x80x", b"\xc0\xaf", b"\xf4\x90\x80\x80",
+                                 "\u00e9\u4e2d\U0001F600".encode()])
+def test_client_request_bytes_for_non_utf8_messages(raw):
+    """A message given as bytes that are not valid UTF-8 (a Go string can
+    hold any bytes): the C++ client's Request is byte-identical to the Python
+    mirror's, i.e. Go's encoding/json output (each invalid byte as \\ufffd,
+    valid UTF-8 raw)."""
+    peer = Peer()
+    p = _run_client(peer.port, raw, 9, "--epoch-millis", "100", "--epoch-limit", "50")
+    try:
+        assert peer.recv() == lsp.NewConnect().marshal()
+        peer.send(lsp.NewAck(7, 0).marshal())
+        want = NewRequest(raw.decode("utf-8", "surrogateescape"), 0, 9).marshal()
+        assert peer.recv(lsp.MsgData) == lsp.NewData(7, 1, want).marshal()
+    finally:
+        p.kill()
+        p.communicate()
+        peer.close()
+
+
 def test_client_resends_each_epoch_then_disconnects():
     peer = Peer()
     t0 = time.monotonic()

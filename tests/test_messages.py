@@ -71,3 +71,14 @@ def test_invalid_utf8_becomes_replacement_char_like_go():
     back = Message.unmarshal(wire)
     assert back.Data == "caf�"
     assert back.Data.encode() == b"caf\xef\xbf\xbd"
+
+
+def test_invalid_utf8_wire_bytes_are_gos():
+    """The bytes on the wire are Go's: each invalid byte is written as the
+    escape \\ufffd (encoding/json), a valid U+FFFD stays raw UTF-8 -- the
+    same bytes the C++ mirror (include/bm_json.hpp) writes."""
+    data = b"a\xe2\x82b\xff".decode("utf-8", "surrogateescape")  # truncated 3-byte sequence, stray 0xff
+    assert NewRequest(data, 0, 1).marshal() == (
+        b'{"Type":1,"Data":"a\\ufffd\\ufffdb\\ufffd","Lower":0,"Upper":1,"Hash":0,"Nonce":0}')
+    assert NewRequest("\ufffd", 0, 1).marshal() == (
+        b'{"Type":1,"Data":"\xef\xbf\xbd","Lower":0,"Upper":1,"Hash":0,"Nonce":0}')
