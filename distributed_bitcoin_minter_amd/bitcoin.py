@@ -12,6 +12,7 @@
 """
 import enum
 import json
+import re
 from dataclasses import dataclass
 
 from . import _lib
@@ -29,8 +30,22 @@ def _ctx():
 
 
 def _as_bytes(msg) -> bytes:
-    # Go's "%s" prints a string's raw bytes; a Python str is taken as UTF-8.
-    return msg.encode() if isinstance(msg, str) else bytes(msg)
+    # Go's "%s" prints a string's raw bytes; a Python str is taken as UTF-8,
+    # with the raw bytes of a surrogateescape-decoded str (argv) restored.
+    return msg.encode("utf-8", "surrogateescape") if isinstance(msg, str) else bytes(msg)
+
+
+_SURROGATE = re.compile("[\ud800-\udfff]")
+
+
+def _go_decoded(s: str) -> str:
+    """What Go's json.Unmarshal leaves in a string: "invalid UTF-8 or invalid
+    UTF-16 surrogate pairs are not treated as an error. Instead, they are
+    replaced by the Unicode replacement character U+FFFD."  Here an invalid
+    raw byte arrives as a surrogateescape surrogate (one per byte, as Go's
+    utf8.DecodeRune yields one RuneError per byte) and a lone \\uD8xx escape
+    as a lone surrogate: both become U+FFFD."""
+    return _SURROGATE.sub("\ufffd", s)
 
 
 def Hash(msg, nonce: int) -> int:
@@ -98,9 +113,14 @@ class Message:
         values; a field of the wrong JSON type is an error, as in Go (Data a
         string; Type an int; Lower/Upper/Hash/Nonce integers in uint64 range,
         no floats, no booleans).  Anything else raises ValueError."""
+        if isinstance(raw, (bytes, bytearray, memoryview)):
+            # Go decodes the payload as UTF-8 without rejecting invalid bytes
+            # inside strings (they become U+FFFD, _go_decoded); outside a
+            # string they are a syntax error either way
+            raw = bytes(raw).decode("utf-8", "surrogateescape")
         try:
             d = json.loads(raw)
-        except (UnicodeDecodeError, RecursionError) as e:
+        except RecursionError as e:
             raise ValueError(f"not a JSON message: {e!r}") from None
         if not isinstance(d, dict):
             raise ValueError("bitcoin message is not a JSON object")
@@ -120,6 +140,7 @@ class Message:
             data = ""
         if not isinstance(data, str):
             raise ValueError("Data is not a string")
+        data = _go_decoded(data)
         return cls(Type=MsgType(num("Type", -(1 << 63), (1 << 63) - 1)), Data=data,
                    Lower=num("Lower", 0, U64_MAX), Upper=num("Upper", 0, U64_MAX),
                    Hash=num("Hash", 0, U64_MAX), Nonce=num("Nonce", 0, U64_MAX))

@@ -173,9 +173,15 @@ class Reader {
                 }
                 continue;
             }
-            // raw bytes must be valid UTF-8 (as the Python mirror requires)
+            // an invalid raw byte becomes U+FFFD, one per byte, as Go's
+            // json.Unmarshal does ("invalid UTF-8 ... replaced by the Unicode
+            // replacement character"; utf8.DecodeRune's width-1 RuneError)
             const auto [r, size] = decode_rune(s_, i_);
-            if (r == 0xFFFD && size == 1) fail("invalid UTF-8");
+            if (r == 0xFFFD && size == 1) {
+                put_utf8(out, 0xFFFD);
+                i_ += 1;
+                continue;
+            }
             out.append(s_.substr(i_, size));
             i_ += size;
         }

@@ -80,7 +80,10 @@ def test_unmarshal_accepts_what_python_accepts():
              b'{"Type":2,"Hash":5,"Extra":[1,{"x":null},"s",true,-1.5e3]}',
              b'{"Type":1,"Data":null,"Lower":null,"Upper":7}',
              b'{"Type":1,"Data":"\\ud83d\\ude00 \\/ \\b\\f","Upper":-0}',
-             b'{"Type":1,"Data":"dup","Data":"last"}', b'{}', b'{"Type":0}']
+             b'{"Type":1,"Data":"dup","Data":"last"}', b'{}', b'{"Type":0}',
+             # invalid UTF-8 inside strings and lone surrogate escapes: U+FFFD, as Go's json.Unmarshal
+             b'{"Type":1,"Data":"a\xffb\xed\xa0\x80c\\ud800d\\udc00","Upper":5}',
+             b'{"Type":2,"X":"\xfe\xc0\xaf","Hash":3}', b'{"Type":1,"Data":"\xf4\x90\x80\x80\xe2\x82"}']
     got = _selftest(cases)
     for raw, out in zip(cases, got):
         assert out == Message.unmarshal(raw).marshal(), raw
@@ -89,7 +92,7 @@ def test_unmarshal_accepts_what_python_accepts():
 def test_unmarshal_rejects_what_python_rejects():
     from test_messages import BAD_PAYLOADS
     extra = [b'{"Type":1,"Data":"a\tb"}', b'{"Type":1} x', b'{"Type":01}', b'{"Type":1,"Upper":18446744073709551616}',
-             b'{"Type":1,"Data":"\xff"}', b'{"Type":1,"Data":"\\x"}', b'{"Type":1,}']
+             b'{"Type":1,"Data":"\\x"}', b'{"Type":1,}', b'{"Type":1,"Data":"x"}\xff', b'\xef\xbb\xbf{"Type":1}']
     bad = BAD_PAYLOADS + extra  # one message per line: none holds a newline
     for b in bad:
         with pytest.raises(ValueError):

@@ -82,3 +82,27 @@ def test_invalid_utf8_wire_bytes_are_gos():
         b'{"Type":1,"Data":"a\\ufffd\\ufffdb\\ufffd","Lower":0,"Upper":1,"Hash":0,"Nonce":0}')
     assert NewRequest("\ufffd", 0, 1).marshal() == (
         b'{"Type":1,"Data":"\xef\xbf\xbd","Lower":0,"Upper":1,"Hash":0,"Nonce":0}')
+
+
+def test_unmarshal_replaces_invalid_utf8_like_go():
+    """json.Unmarshal: "invalid UTF-8 or invalid UTF-16 surrogate pairs are
+    not treated as an error. Instead, they are replaced by the Unicode
+    replacement character U+FFFD" -- one per invalid byte (utf8.DecodeRune),
+    one per lone surrogate escape.  A Go miner then hashes U+FFFD's bytes
+    (EF BF BD), and so does ours.  Invalid bytes outside a string, or a BOM,
+    stay syntax errors."""
+    m = Message.unmarshal(b'{"Type":1,"Data":"a\xffb\xed\xa0\x80c\\ud800d\\ud83d\\ude00","Upper":5}')
+    assert m.Data == "a\ufffdb\ufffd\ufffd\ufffdc\ufffdd\U0001F600"
+    from distributed_bitcoin_minter_amd.bitcoin import _as_bytes
+    assert _as_bytes(m.Data) == b"a\xef\xbf\xbdb" + b"\xef\xbf\xbd" * 3 + b"c\xef\xbf\xbdd\xf0\x9f\x98\x80"
+    for bad in (b'{"Type":1}\xff', b'\xef\xbb\xbf{"Type":1}', b'{"Type":1,"Data":"x\x01"}'):
+        with pytest.raises(ValueError):
+            Message.unmarshal(bad)
+
+
+def test_raw_bytes_of_an_argv_string_are_hashed_as_is():
+    """Go's %s prints a string's bytes; a Python str decoded from argv with
+    surrogateescape gives its original bytes back to the search."""
+    from distributed_bitcoin_minter_amd.bitcoin import _as_bytes
+    assert _as_bytes(b"caf\xe9".decode("utf-8", "surrogateescape")) == b"caf\xe9"
+    assert _as_bytes("caf\u00e9") == b"caf\xc3\xa9"
