@@ -10,10 +10,11 @@ or, if the connection to the server is lost (or cannot be made),
 
     Disconnected                    (printDisconnected, client.go:81-83)
 
-and exits.  maxNonce is parsed as an unsigned 64-bit integer (client.go:25
-uses ParseInt; the spec's nonces are uint64).
+and exits.  maxNonce is parsed as Go's strconv.ParseUint(s, 10, 64) would
+(client.go:25 uses ParseInt; the spec's nonces are uint64).
 """
 import argparse
+import re
 import sys
 
 from . import lsp
@@ -56,10 +57,9 @@ def main(argv=None, out=None):
     ap.add_argument("--epoch-millis", type=int, default=lsp.DefaultEpochMillis)
     ap.add_argument("--window-size", type=int, default=lsp.DefaultWindowSize)
     a = ap.parse_args(argv)
-    try:
-        max_nonce = int(a.maxNonce, 10)
-    except ValueError:
-        max_nonce = -1
+    # strconv.ParseUint(s, 10, 64): ASCII digits only (no sign, spaces or
+    # underscores, which Python's int() would take), at most 2^64-1
+    max_nonce = int(a.maxNonce) if re.fullmatch(r"[0-9]+", a.maxNonce, flags=re.ASCII) else -1
     if not 0 <= max_nonce <= U64_MAX:
         print(f"maxNonce must be an unsigned 64-bit integer, got {a.maxNonce!r}", file=sys.stderr)
         return 2

@@ -40,7 +40,10 @@ int main(int argc, char** argv) {
     errno = 0;
     char* end = nullptr;
     const unsigned long long max_nonce = std::strtoull(pos[2].c_str(), &end, 10);
-    if (pos[2].empty() || pos[2][0] == '-' || *end || errno == ERANGE) {
+    // strconv.ParseUint(s, 10, 64): digits only (strtoull alone would take
+    // leading spaces and a sign)
+    const bool digits = !pos[2].empty() && pos[2].find_first_not_of("0123456789") == std::string::npos;
+    if (!digits || *end || errno == ERANGE) {
         std::fprintf(stderr, "maxNonce must be an unsigned 64-bit integer, got '%s'\n", pos[2].c_str());
         return 2;
     }

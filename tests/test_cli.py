@@ -73,3 +73,12 @@ def test_miner_process_without_gpu_fails_loudly():
     m = py(f"{PKG}.miner", "127.0.0.1:9", *FAST, env=dict(os.environ))
     _, err = m.communicate(timeout=60)
     assert m.returncode != 0 and "no usable gfx950 device" in err
+
+
+def test_client_rejects_max_nonce_go_would_reject():
+    """maxNonce as strconv.ParseUint(s, 10, 64): ASCII digits only, at most
+    2^64-1 (Python's int() alone would take spaces, a sign, underscores and
+    other scripts' digits).  Leading zeros are fine, as in Go."""
+    from distributed_bitcoin_minter_amd import client
+    for bad in ("-1", "18446744073709551616", "12x", "", " 5", "+5", "5_0", "0x10", "٥"):
+        assert client.main(["127.0.0.1:1", "m", bad]) == 2, bad

@@ -143,7 +143,7 @@ def test_client_no_answer_to_connect():
 
 
 def test_client_rejects_bad_max_nonce():
-    for bad in ("-1", "18446744073709551616", "12x", ""):
+    for bad in ("-1", "18446744073709551616", "12x", "", " 5", "+5", "5_0", "0x10", "\u0665"):
         r = subprocess.run([_client(), "127.0.0.1:1", "m", bad], capture_output=True, timeout=30)
         assert r.returncode == 2, bad
 
