@@ -140,7 +140,7 @@ except ImportError:  # pragma: no cover - hypothesis is in the image
     given = None
 
 if given is not None:
-    @settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+    @settings(max_examples=200, deadline=None, derandomize=True, suppress_health_check=[HealthCheck.too_slow])
     @given(msg=st.binary(min_size=0, max_size=200),
            lo=st.one_of(st.integers(0, 10 ** 6), st.integers(0, U64),
                         st.sampled_from([10 ** k - 3 for k in range(1, 20)])),
