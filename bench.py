@@ -60,7 +60,9 @@ Also reported:
   cpu_baseline  the oracle's loop shape (format + SHA-256 + strict '<') on this
                 host's cores over a bounded sample of C2 (rank 0, N = 1 only);
                 "system": one LSP server + N single-threaded CPU miner processes
-                + a client over the same window.
+                + a client over the same window; "optimized": the oracle's
+                16-lane AVX-512 scan (a tuned CPU, not the reference's loop) on
+                the same cores and window.
 """
 import argparse
 import glob
