@@ -47,13 +47,27 @@ ranks / that time.  The answer is checked against the committed golden
 (tests/golden/) for the workload; a wrong answer exits non-zero.
 
 Also reported:
-  roofline      the dominant launch: algorithmic int32 ops (nonces x C x 1384,
-                SURVEY.md §8d, C = SHA-256 blocks the kernel compresses per
-                nonce) / its HIP-event time on the library's stream, vs 78.64 T
-                lane-ops/s per GPU; the issue bound of the kernel's loop at
-                the clock measured on this box after the timed region
-                (measure_clock); PMC figures (VALU per nonce, memory-side
-                bytes) from profiles/<round>/ for the same config.
+  roofline      the dominant launch, three ways:
+                frac       canonical: algorithmic int32 ops (nonces x C x
+                           1384, SURVEY.md §8d, C = SHA-256 blocks the kernel
+                           compresses per nonce) / its HIP-event time on the
+                           library's stream, vs 78.64 T lane-ops/s per GPU --
+                           the metric's own figure, not a ceiling (it can
+                           exceed 1 where constant words fold away);
+                executed   the VALU lane-ops the kernel really executes per
+                           nonce (PMC SQ_INSTS_VALU, else the static count)
+                           over the same time, vs 78.64 T and vs the peak at
+                           the clock measured under the kernel on this box;
+                issue_bound  the ceiling: the kernel loop's issue bound at
+                           that clock (measure_clock), and the fraction of
+                           it reached;
+                plus PMC memory-side bytes from profiles/<round>/.
+  rccl_nranks / scaling_valid  (N > 1) what RCCL reported about the
+                communicator (ncclCommCount, per rank or device its
+                ncclCommUserRank and ncclCommCuDevice, beside each GPU's PCI
+                bus id), and whether the line measured N distinct GPUs
+                combined the way the run asked for (false, with reasons, on a
+                fallback or a one-GPU rehearsal).
   config.ranks / config.devices
                 each rank's (device's) nonces, GPU span and rate, and the
                 combine that ran.
@@ -172,6 +186,29 @@ def issue_bound(p, nbv, clock_ghz):
     return {"valu_per_nonce": lay["valu"], "slow": lay["valu_slow"], "fast": lay["valu_fast"],
             "issue_slots_per_nonce": lay["issue_slots"], "clock_ghz": round(clock_ghz, 3),
             "GHs_per_gpu": round(ghs, 2)}
+
+
+def executed_roofline(nonces, kernel_ms, valu_pmc, pmc_src, valu_static, clock_ghz):
+    """The dominant launch against the VALU peak in the instructions it
+    really executes: VALU lane-ops per nonce (rocprofv3 SQ_INSTS_VALU x 64 /
+    nonces from the committed PMC pass of this config, else the static count
+    of the built inner loop, isa_mix.json) x nonces / launch time, as a
+    fraction of 78.64 T (2.4 GHz) and of the peak at the clock measured under
+    the kernel on this box.  The ceiling for this loop is its issue bound
+    (issue_bound.frac); this fraction is below 1 by construction."""
+    if valu_pmc:
+        v, src = valu_pmc, f"PMC SQ_INSTS_VALU x 64 / nonces ({pmc_src})"
+    elif valu_static:
+        v, src = valu_static, "static count of the built inner loop (isa_mix.json)"
+    else:
+        return None
+    ach = nonces * v / (kernel_ms * 1e-3) / 1e12
+    out = {"valu_per_nonce": v, "src": src, "achieved": round(ach, 3), "unit": "T int32 lane-ops/s",
+           "frac": round(ach / VALU_PEAK_T, 4)}
+    if clock_ghz:
+        peak = VALU_PEAK_T * clock_ghz / 2.4
+        out.update(peak_live=round(peak, 2), clock_ghz=round(clock_ghz, 3), frac_live_clock=round(ach / peak, 4))
+    return out
 
 
 class ClockSampler:
@@ -453,6 +490,93 @@ def calibrate_split(args, ctx, grp):
             "rates_nonces_per_ms": [round(r, 1) for r in rates]}
 
 
+def _mean(xs):
+    return sum(xs) / len(xs) if xs else 0.0
+
+
+def pci_bus_id(device):
+    """The device's PCI bus id (names the physical GPU across processes, whose
+    HIP device numbers depend on their visibility masks), or None."""
+    try:
+        return device_pci_bus_id(device)
+    except Exception:  # noqa: BLE001 -- informational
+        return None
+
+
+def step_record(st):
+    """What the line keeps of one call's bm_stats_t: nonces, GPU span, the
+    combine that ran and RCCL's view of the communicator, per device too."""
+    return {"nonces": st.nonces, "span_ms": st.span_ms, "combine": COMBINED_NAMES.get(st.combine_used, "?"),
+            "rccl_status": st.rccl_status, "rccl_nranks": st.rccl_nranks, "rccl_rank": st.rccl_rank,
+            "devices": [(st.dev_nonces[i], st.dev_span_ms[i]) for i in range(st.devices)],
+            "dev_rccl": [(st.dev_rccl_rank[i], st.dev_rccl_device[i]) for i in range(st.devices)]}
+
+
+def rank_summary(rank, dev, pers, sysfs_clock):
+    """One torchrun rank's share of the timed steps (pers: step() records):
+    its GPU (HIP device and PCI bus id), nonces, GPU span and rate, the
+    combine that ran, what RCCL reported about the communicator
+    (ncclCommCount / ncclCommUserRank / ncclCommCuDevice; 0 / -1 without
+    one), and its GPU clock over the timed region."""
+    last = pers[-1]
+    mine = {"rank": rank, "device": dev, "pci_bus_id": pci_bus_id(dev), "nonces": last["nonces"],
+            "span_ms": round(_mean([p["span_ms"] for p in pers]), 3), "combine": last["combine"],
+            "rccl_nranks": last["rccl_nranks"], "rccl_rank": last["rccl_rank"],
+            "rccl_device": last["dev_rccl"][0][1] if last["dev_rccl"] else -1,
+            "clock_ghz_sysfs": None if sysfs_clock is None else round(sysfs_clock, 3)}
+    mine["GHs"] = round(mine["nonces"] / mine["span_ms"] / 1e6, 3) if mine["span_ms"] > 0 else None
+    if last["rccl_status"]:
+        mine["rccl_status"] = last["rccl_status"]
+    return mine
+
+
+def device_summaries(pers, device_ids):
+    """Per device of a one-process context: its HIP device and PCI bus id,
+    nonces, span and rate, and its rank in the context's RCCL communicator
+    (with the device RCCL placed that rank on)."""
+    last = pers[-1]
+    slots = []
+    for i, (nn, _sp) in enumerate(last["devices"]):
+        sp = _mean([p["devices"][i][1] for p in pers])
+        r, d = last["dev_rccl"][i] if i < len(last["dev_rccl"]) else (-1, -1)
+        slots.append({"device": device_ids[i], "pci_bus_id": pci_bus_id(device_ids[i]), "nonces": nn,
+                      "span_ms": round(sp, 3), "GHs": round(nn / sp / 1e6, 3) if sp > 0 else None,
+                      "combine": last["combine"], "rccl_nranks": last["rccl_nranks"], "rccl_rank": r,
+                      "rccl_device": d})
+    return slots
+
+
+def scaling_validity(n, slots, want, rehearsal):
+    """Whether an N > 1 line measures what it claims: N slots (ranks or
+    devices) on N distinct physical GPUs (PCI bus ids), combined the way the
+    run asked for -- want = "rccl": every slot combined through one RCCL
+    communicator that RCCL itself says has N ranks, numbered 0..N-1; "gather":
+    every rank's own partial met over the rendezvous.  A fallback (e.g. a
+    group that could not form) or a rehearsal on one GPU makes it false, with
+    the reasons listed."""
+    why = []
+    if rehearsal:
+        why.append("rehearsal: every rank / device is GPU 0")
+    if len(slots) != n:
+        why.append(f"{len(slots)} ranks / devices reported for {n} GPUs")
+    buses = [s.get("pci_bus_id") for s in slots]
+    if any(b is None for b in buses) or len(set(buses)) != len(buses):
+        why.append(f"{len({b for b in buses if b})} distinct GPUs (PCI bus ids) under {len(buses)} ranks / devices")
+    combines = sorted({s["combine"] for s in slots})
+    if want == "rccl":
+        if combines != ["rccl"]:
+            why.append(f"combine {'/'.join(combines)} instead of one RCCL allgather")
+        else:
+            counts = sorted({s["rccl_nranks"] for s in slots})
+            if counts != [n]:
+                why.append(f"RCCL communicator of {counts} ranks, not {n}")
+            if sorted(s["rccl_rank"] for s in slots) != list(range(n)):
+                why.append(f"RCCL ranks {sorted(s['rccl_rank'] for s in slots)}, not 0..{n - 1}")
+    elif combines != ["local"]:
+        why.append(f"combine {'/'.join(combines)} instead of the rendezvous gather of own partials")
+    return {"scaling_valid": not why, "scaling_invalid": why} if why else {"scaling_valid": True}
+
+
 JOIN_TIMEOUT_MS = 120_000  # a group that has not formed by then falls back to the rendezvous gather
 PEER_TIMEOUT_MS = 120_000  # a joined rank waits at most this long for the others' partials
 
@@ -590,10 +714,7 @@ def main():
         # this device's algorithmic ops over the call's GPU span (first
         # launch start to last launch end): launches overlap on two streams
         ops = sum(L.nonces * kernel_compressions(L) for L in launches) * OPS_PER_COMPRESSION
-        per = {"nonces": st.nonces, "span_ms": st.span_ms, "combine": COMBINED_NAMES.get(st.combine_used, "?"),
-               "rccl_status": st.rccl_status,
-               "devices": [(st.dev_nonces[i], st.dev_span_ms[i]) for i in range(st.devices)]}
-        return res, (dom, ops, st.span_ms, per)
+        return res, (dom, ops, st.span_ms, step_record(st))
 
     for _ in range(args.warmup):
         step()
@@ -629,21 +750,12 @@ def main():
     mean = lambda xs: sum(xs) / len(xs) if xs else 0.0
     if world > 1:
         # each rank's share of the timed steps: its nonces, its GPU span, its
-        # rate, how the partials met, and its GPU clock (driver hwmon)
-        mine = {"rank": grp.rank, "device": dev, "nonces": pers[-1]["nonces"],
-                "span_ms": round(mean([p["span_ms"] for p in pers]), 3), "combine": combine,
-                "clock_ghz_sysfs": None if sysfs_clock is None else round(sysfs_clock, 3)}
-        mine["GHs"] = round(mine["nonces"] / mine["span_ms"] / 1e6, 3) if mine["span_ms"] > 0 else None
-        if pers[-1]["rccl_status"]:
-            mine["rccl_status"] = pers[-1]["rccl_status"]
-        slots = grp.gather(mine)
+        # rate, how the partials met (and what RCCL says about the
+        # communicator), and its GPU clock (driver hwmon)
+        slots = grp.gather(rank_summary(grp.rank, dev, pers, sysfs_clock))
         how += f"; combine {combine}"
     else:
-        slots = []
-        for i, (nn, _sp) in enumerate(pers[-1]["devices"]):
-            sp = mean([p["devices"][i][1] for p in pers])
-            slots.append({"device": i, "nonces": nn, "span_ms": round(sp, 3),
-                          "GHs": round(nn / sp / 1e6, 3) if sp > 0 else None})
+        slots = device_summaries(pers, ([0] * n if args.rehearse_one_gpu else list(range(n))) if n > 1 else [dev])
         if n > 1:
             how += f"; combine {combine}" + (f" (RCCL failed, status {pers[-1]['rccl_status']}: host copies)"
                                              if pers[-1]["rccl_status"] else "")
@@ -668,6 +780,13 @@ def main():
         "result_ok": None if want is None else list(res) == want,
         "hip_runtime": hip_runtimes(),
     }
+    if n > 1:
+        # what RCCL itself reported (ncclCommCount / UserRank / CuDevice per
+        # rank or device) and whether the line measures N distinct GPUs
+        # combined the way the run asked for
+        out["rccl_nranks"] = (sorted({s["rccl_nranks"] for s in slots}) if world > 1
+                              else pers[-1]["rccl_nranks"])
+        out.update(scaling_validity(n, slots, args.combine if world > 1 else "rccl", args.rehearse_one_gpu))
     if dom is not None:
         ms = [d[0].ms for d in doms if d[0] is not None]
         dom_ms = sum(ms) / len(ms)
@@ -680,6 +799,10 @@ def main():
         clock = pmc.get("clock_ghz")
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_T, 2),
                 "unit": "T int32 lane-ops/s", "frac": round(achieved / VALU_PEAK_T, 4),
+                "frac_basis": "canonical: SURVEY.md §8d's 1,384 int32 ops per compression x the blocks the "
+                              "kernel compresses per nonce; not a ceiling -- the kernel executes fewer ops per "
+                              "nonce than that count (see executed), so this can exceed 1 on layouts whose "
+                              "constant words fold away (DESIGN.md §5)",
                 "traffic": pmc.get("hbm_bytes_per_launch"),
                 "traffic_unit": "memory-side bytes per launch (PMC FETCH_SIZE+WRITE_SIZE)",
                 "traffic_note": "memory-side writes of the dequeue counter's returning atomics and of the rare "
@@ -739,7 +862,11 @@ def main():
             else:
                 ib["clock_src"] = pmc_src
                 ib["note"] = "no clock measured on this box: the bound at the committed PMC clock, no frac"
+            ib["role"] = "ceiling: the loop's own issue bound at the measured clock (DESIGN.md §5)"
             roof["issue_bound"] = ib
+        static = issue_bound(dom.p, dom.nbv, 1.0)  # the built loop's static VALU count
+        roof["executed"] = executed_roofline(dom.nonces, dom_ms, roof.get("valu_per_nonce_pmc"), pmc_src,
+                                             static and static["valu_per_nonce"], ib_clock)
         if calls:
             # the whole call on this device: every launch's algorithmic ops over
             # the span of its launches (two streams overlap launches, which

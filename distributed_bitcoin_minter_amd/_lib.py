@@ -24,7 +24,7 @@ BM_ETIMEDOUT = -8
 BM_MAX_LAUNCH_STATS = 64
 BM_MAX_STAT_DEVICES = 16
 BM_RCCL_ID_BYTES = 128
-BM_ABI_VERSION = 5
+BM_ABI_VERSION = 6
 BM_COMBINE_AUTO, BM_COMBINE_RCCL, BM_COMBINE_HOST = 0, 1, 2
 # bm_stats_t.combine_used
 BM_COMBINED_NONE, BM_COMBINED_RCCL, BM_COMBINED_HOST, BM_COMBINED_LOCAL = 0, 1, 2, 3
@@ -51,7 +51,8 @@ class Stats(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double), ("span_ms", ctypes.c_double), ("nonces", c_u64),
                 ("combine_used", c_i32), ("rccl_status", c_i32), ("devices", c_u32), ("reserved", c_u32),
                 ("dev_nonces", c_u64 * BM_MAX_STAT_DEVICES), ("dev_span_ms", ctypes.c_double * BM_MAX_STAT_DEVICES),
-                ("launch", LaunchStat * BM_MAX_LAUNCH_STATS)]
+                ("rccl_nranks", c_i32), ("rccl_rank", c_i32), ("dev_rccl_rank", c_i32 * BM_MAX_STAT_DEVICES),
+                ("dev_rccl_device", c_i32 * BM_MAX_STAT_DEVICES), ("launch", LaunchStat * BM_MAX_LAUNCH_STATS)]
 
 
 class Segment(ctypes.Structure):

@@ -58,8 +58,13 @@ def main(argv=None, out=None):
     ap.add_argument("--window-size", type=int, default=lsp.DefaultWindowSize)
     a = ap.parse_args(argv)
     # strconv.ParseUint(s, 10, 64): ASCII digits only (no sign, spaces or
-    # underscores, which Python's int() would take), at most 2^64-1
-    max_nonce = int(a.maxNonce) if re.fullmatch(r"[0-9]+", a.maxNonce, flags=re.ASCII) else -1
+    # underscores, which Python's int() would take), at most 2^64-1 (leading
+    # zeros allowed); more than 20 significant digits is out of range before
+    # int() sees it (Python refuses > 4300-digit strings with ValueError)
+    max_nonce = -1
+    if re.fullmatch(r"[0-9]+", a.maxNonce, flags=re.ASCII):
+        digits = a.maxNonce.lstrip("0") or "0"
+        max_nonce = int(digits) if len(digits) <= 20 else -1
     if not 0 <= max_nonce <= U64_MAX:
         print(f"maxNonce must be an unsigned 64-bit integer, got {a.maxNonce!r}", file=sys.stderr)
         return 2

@@ -96,6 +96,18 @@ struct Launch {
     bm_launch_stat_t stat;
 };
 
+// bm_ctx_join_rank's worker: one communicator set-up, shared with the caller
+// (who may give up on it: then the worker aborts what it made).  A join the
+// caller gave up on stays on the context as its pending join, so a context
+// never has more than one worker inside RCCL.
+struct JoinJob {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclComm_t comm = nullptr;
+    int rc = BM_ERCCL;
+};
+
 namespace {
 int hip_status(hipError_t e) { return e == hipSuccess ? BM_OK : BM_EHIP; }
 
@@ -153,6 +165,10 @@ struct bm_ctx {
     uint64_t lane_chunk = bm::kNoncesPerLaneChunk;  // nonces per lane per dequeue, at most (BTCMINER_CHUNK)
     std::vector<uint32_t> shares;  // the partitioner's shares per slot (empty: near-equal pieces)
     bool balance = false;          // multi-device: shares follow each device's measured rate
+    // rank ctx: a join whose caller timed out while its worker was still
+    // inside RCCL (the worker aborts the communicator if it ever gets one)
+    std::shared_ptr<bm::JoinJob> pending_join;
+    std::thread pending_worker;
     bm_stats_t stats;
 };
 
@@ -300,7 +316,10 @@ void destroy_device(DeviceCtx& d) {
     if (d.stream) (void)hipStreamSynchronize(d.stream);
     for (auto& s : d.aux)
         if (s) (void)hipStreamSynchronize(s);
-    if (d.comm) (void)ncclCommDestroy(d.comm);
+    // abort, not destroy: the streams are drained, so nothing of ours is in
+    // flight, and an abort never waits on a peer (a joined rank whose group
+    // lost a member would otherwise block in teardown)
+    if (d.comm) (void)ncclCommAbort(d.comm);
     d.comm = nullptr;
     for (auto& e : d.ev)
         if (e) (void)hipEventDestroy(e);
@@ -368,16 +387,6 @@ int comm_settle(ncclComm_t comm, ncclResult_t r, std::chrono::steady_clock::time
     }
     return r == ncclSuccess ? BM_OK : BM_ERCCL;
 }
-
-// bm_ctx_join_rank's worker: one communicator set-up, shared with the caller
-// (who may give up on it: then the worker aborts what it made).
-struct JoinJob {
-    std::mutex m;
-    std::condition_variable cv;
-    bool done = false, abandoned = false;
-    ncclComm_t comm = nullptr;
-    int rc = BM_ERCCL;
-};
 
 void join_worker(std::shared_ptr<JoinJob> job, int dev, int world, int rank, ncclUniqueId u) {
     ncclComm_t comm = nullptr;
@@ -487,6 +496,32 @@ int enqueue(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches, std::vector
     return BM_OK;
 }
 
+// What RCCL reports about the communicator(s) a combine just ran over, into
+// the stats: its rank count, and each device's rank and the HIP device RCCL
+// placed it on (bm_stats_t.rccl_*).  used = false (no RCCL combine), or a
+// device without a communicator: 0 ranks, -1 elsewhere.
+void record_rccl(bm_ctx* ctx, bool used) {
+    bm_stats_t& st = ctx->stats;
+    for (int i = 0; i < BM_MAX_STAT_DEVICES; ++i) st.dev_rccl_rank[i] = st.dev_rccl_device[i] = -1;
+    st.rccl_nranks = 0;
+    st.rccl_rank = -1;
+    for (size_t di = 0; used && di < ctx->devs.size(); ++di) {
+        ncclComm_t c = ctx->devs[di].comm;
+        int n = 0, r = -1, dev = -1;
+        if (!c || ncclCommCount(c, &n) != ncclSuccess) continue;
+        if (ncclCommUserRank(c, &r) != ncclSuccess) r = -1;
+        if (ncclCommCuDevice(c, &dev) != ncclSuccess) dev = -1;
+        if (di == 0) {
+            st.rccl_nranks = n;
+            st.rccl_rank = r;
+        }
+        if (di < (size_t)BM_MAX_STAT_DEVICES) {
+            st.dev_rccl_rank[di] = r;
+            st.dev_rccl_device[di] = dev;
+        }
+    }
+}
+
 Partial lex_min_slots(const Slot* s, int n) {
     Partial best{UINT64_MAX, UINT64_MAX};
     for (int i = 0; i < n; ++i) {
@@ -563,6 +598,7 @@ int combine_local(bm_ctx* ctx, Partial* best_out) {
     }
     st.combine_used = ctx->rank_ctx ? BM_COMBINED_LOCAL : via_rccl ? BM_COMBINED_RCCL : BM_COMBINED_HOST;
     st.rccl_status = ctx->rccl_status;
+    record_rccl(ctx, via_rccl);
     *best_out = lex_min_slots(ctx->devs[0].h_slots, nslots);
     return BM_OK;
 }
@@ -576,19 +612,28 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
     bm_stats_t& st = ctx->stats;
     DeviceCtx& d = ctx->devs[0];
     const int world = ctx->world;
-    if (hipSetDevice(d.id) != hipSuccess) return BM_EHIP;
-    if (own_rc == BM_OK) {
-        if (hipMemsetAsync(&d.d_slot->status, 0, 2 * sizeof(uint64_t), d.stream) != hipSuccess) return BM_EHIP;
-    } else {
+    // Post this rank's slot.  A HIP failure while staging it becomes this
+    // rank's status (it still takes part, so the group fails the call
+    // together instead of waiting for it); only a slot that cannot be posted
+    // at all leaves the group (abort below).
+    bool posted = hipSetDevice(d.id) == hipSuccess;
+    if (posted && own_rc == BM_OK &&
+        hipMemsetAsync(&d.d_slot->status, 0, 2 * sizeof(uint64_t), d.stream) != hipSuccess)
+        own_rc = BM_EHIP;
+    if (posted && own_rc != BM_OK) {
         Slot& out = d.h_slots[d.nslots];  // pinned staging slot
         out = Slot{Partial{UINT64_MAX, UINT64_MAX}, (uint64_t)(int64_t)own_rc, 0};
-        if (hipMemcpyAsync(d.d_slot, &out, sizeof(Slot), hipMemcpyHostToDevice, d.stream) != hipSuccess)
-            return BM_EHIP;
+        posted = hipMemcpyAsync(d.d_slot, &out, sizeof(Slot), hipMemcpyHostToDevice, d.stream) == hipSuccess;
     }
-    if (hipEventRecord(d.own_done, d.stream) != hipSuccess) return BM_EHIP;
+    // the end of this rank's own work, from which the peer timeout counts
+    // (without the event: from the moment the allgather is enqueued)
+    const bool own_mark = posted && hipEventRecord(d.own_done, d.stream) == hipSuccess;
     const bool limited = ctx->peer_timeout_ms > 0;
     int rc = BM_OK;
-    if (ctx->test_rccl_fault == 2) {
+    bool copied = false;
+    if (!posted) {
+        rc = own_rc != BM_OK ? own_rc : BM_EHIP;
+    } else if (ctx->test_rccl_fault == 2) {
         rc = BM_ERCCL;  // test hook: as if the allgather failed (world 1 only: no peer is left waiting)
     } else {
         // the allgather goes on the stream behind this rank's own work (a
@@ -597,34 +642,34 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
         const auto timeout = std::chrono::milliseconds(ctx->peer_timeout_ms);
         rc = comm_settle(d.comm, ncclAllGather(d.d_slot, d.d_gather, kSlotWords, ncclUint64, d.comm, d.stream),
                          std::chrono::steady_clock::now() + timeout, limited);
-        if (rc == BM_OK && hipMemcpyAsync(d.h_slots, d.d_gather, sizeof(Slot) * world, hipMemcpyDeviceToHost,
-                                          d.stream) != hipSuccess)
-            return BM_EHIP;
-        // the deadline counts from the end of this rank's own work: only the
-        // wait for the other ranks is bounded
-        if (hipEventSynchronize(d.own_done) != hipSuccess) return BM_EHIP;
+        // a failed copy of the gathered slots is this rank's own error: the
+        // collective itself still runs, so the communicator stays good
+        copied = rc == BM_OK && hipMemcpyAsync(d.h_slots, d.d_gather, sizeof(Slot) * world,
+                                               hipMemcpyDeviceToHost, d.stream) == hipSuccess;
+        // only the wait for the other ranks is bounded
+        if (own_mark) (void)hipEventSynchronize(d.own_done);
         const auto deadline = std::chrono::steady_clock::now() + timeout;
-        if (rc == BM_OK && !limited) {
-            if (hipStreamSynchronize(d.stream) != hipSuccess) return BM_EHIP;
-        } else if (rc == BM_OK) {
-            for (auto pause = std::chrono::microseconds(10);;) {
-                const hipError_t q = hipStreamQuery(d.stream);
-                if (q == hipSuccess) break;
-                if (q != hipErrorNotReady) return BM_EHIP;
-                if (std::chrono::steady_clock::now() > deadline) {
-                    rc = BM_ETIMEDOUT;
-                    break;
-                }
-                std::this_thread::sleep_for(pause);
-                pause = std::min(pause * 2, std::chrono::microseconds(100));
+        if (rc == BM_OK && !limited && hipStreamSynchronize(d.stream) != hipSuccess) rc = BM_EHIP;
+        for (auto pause = std::chrono::microseconds(10); rc == BM_OK && limited;) {
+            const hipError_t q = hipStreamQuery(d.stream);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) {
+                rc = BM_EHIP;  // the stream itself failed: the allgather's fate is unknown
+                break;
             }
+            if (std::chrono::steady_clock::now() > deadline) {
+                rc = BM_ETIMEDOUT;
+                break;
+            }
+            std::this_thread::sleep_for(pause);
+            pause = std::min(pause * 2, std::chrono::microseconds(100));
         }
     }
     if (rc != BM_OK) {
         // the communicator cannot be trusted any more: abort it (this also
         // ends an allgather still waiting on the stream); later searches
         // return the same status until bm_ctx_leave_rank
-        (void)ncclCommAbort(d.comm);
+        if (d.comm) (void)ncclCommAbort(d.comm);
         d.comm = nullptr;
         ctx->group_status = rc;
         (void)hipStreamSynchronize(d.stream);
@@ -633,6 +678,8 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
         return own_rc != BM_OK ? own_rc : rc;  // this rank's own failure stays the one it reports
     }
     st.combine_used = BM_COMBINED_RCCL;
+    record_rccl(ctx, true);
+    if (!copied) return own_rc != BM_OK ? own_rc : BM_EHIP;
     for (int r = 0; r < world; ++r)
         if (d.h_slots[r].status != 0) return own_rc != BM_OK ? own_rc : BM_EPEER;
     if (own_rc != BM_OK) return own_rc;
@@ -703,6 +750,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
     const auto t_start = std::chrono::steady_clock::now();
     bm_stats_t& st = ctx->stats;
     std::memset(&st, 0, sizeof st);
+    record_rccl(ctx, false);
     const int ndev = (int)ctx->devs.size();
     const bool group = ctx->rank_ctx && ctx->joined;
     if (group && ctx->group_status != BM_OK) {  // the communicator failed earlier: leave the group first
@@ -732,6 +780,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
             drain(ctx);
             const int keep = st.rccl_status;
             std::memset(&st, 0, sizeof st);
+            record_rccl(ctx, false);
             st.rccl_status = keep;
             return grc;
         }
@@ -740,6 +789,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         if (rc != BM_OK) {
             drain(ctx);
             std::memset(&st, 0, sizeof st);
+            record_rccl(ctx, false);
             return rc;
         }
     }
@@ -951,6 +1001,7 @@ int create_ctx(const int* devices, int n, int nslots, bm_ctx** out) {
     bm_ctx* ctx = new (std::nothrow) bm_ctx();
     if (!ctx) return BM_ENOMEM;
     std::memset(&ctx->stats, 0, sizeof ctx->stats);
+    record_rccl(ctx, false);
     read_env(ctx);
     DeviceGuard guard;
     ctx->devs.resize(n);
@@ -1004,14 +1055,30 @@ int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
     if (hipSetDevice(d.id) != hipSuccess) return BM_EHIP;
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
+    const int dev = d.id, world = ctx->world, rank = ctx->rank;
+    // An earlier join this context gave up on may still be inside RCCL: wait
+    // for it (within this call's timeout) rather than put a second worker
+    // there; it has abandoned = true, so it aborts whatever it ends with.
+    if (ctx->pending_join) {
+        auto& pj = ctx->pending_join;
+        std::unique_lock<std::mutex> lk(pj->m);
+        const bool ended = timeout_ms == 0 ? (pj->cv.wait(lk, [&] { return pj->done; }), true)
+                                           : pj->cv.wait_for(lk, std::chrono::milliseconds(timeout_ms),
+                                                             [&] { return pj->done; });
+        lk.unlock();
+        if (!ended) {
+            bm::trace("rank %d: the previous join is still inside RCCL; not starting another", rank);
+            return BM_ETIMEDOUT;
+        }
+        ctx->pending_worker.join();
+        ctx->pending_join.reset();
+    }
     // The join runs on a worker thread: a non-blocking ncclCommInitRankConfig
     // polled until it settles.  With a timeout the caller waits at most that
-    // long; past it the worker is left to abort the communicator in the
-    // background (neither the init of a group whose peer never comes nor
-    // its abort is guaranteed to return promptly), and the call returns
-    // BM_ETIMEDOUT.
+    // long; past it the worker becomes the context's pending join (neither
+    // the init of a group whose peer never comes nor its abort is guaranteed
+    // to return promptly), and the call returns BM_ETIMEDOUT.
     auto job = std::make_shared<bm::JoinJob>();
-    const int dev = d.id, world = ctx->world, rank = ctx->rank;
     bm::trace("rank %d/%d: joining (timeout %d ms)", rank, world, timeout_ms);
     std::thread worker([job, dev, world, rank, u]() { bm::join_worker(job, dev, world, rank, u); });
     std::unique_lock<std::mutex> lk(job->m);
@@ -1020,8 +1087,9 @@ int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
     } else if (!job->cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return job->done; })) {
         job->abandoned = true;
         lk.unlock();
-        worker.detach();
-        bm::trace("rank %d: join timed out; the communicator is aborted in the background", rank);
+        ctx->pending_join = job;
+        ctx->pending_worker = std::move(worker);
+        bm::trace("rank %d: join timed out; the worker aborts the communicator if it ever gets one", rank);
         return BM_ETIMEDOUT;
     }
     lk.unlock();
@@ -1098,6 +1166,19 @@ int bm_ctx_create(int num_gpus, bm_ctx_t** out) {
 
 int bm_ctx_destroy(bm_ctx_t* ctx) {
     if (!ctx) return BM_EINVAL;
+    if (ctx->pending_join) {
+        // a join worker that has ended is joined; one still blocked inside
+        // RCCL holds only its JoinJob, so it is left to end with the process
+        bool ended;
+        {
+            std::lock_guard<std::mutex> g(ctx->pending_join->m);
+            ended = ctx->pending_join->done;
+        }
+        if (ended)
+            ctx->pending_worker.join();
+        else
+            ctx->pending_worker.detach();
+    }
     bm::DeviceGuard guard;
     for (auto& d : ctx->devs) bm::destroy_device(d);
     delete ctx;

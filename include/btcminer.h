@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BM_ABI_VERSION 5
+#define BM_ABI_VERSION 6
 
 /* status codes */
 #define BM_OK 0
@@ -104,20 +104,34 @@ int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out);
  *      bytes to every rank, and each calls bm_ctx_join_rank(): a
  *      non-blocking ncclCommInitRankConfig on a worker thread; the call
  *      waits for it at most timeout_ms (0: no limit) and then returns
- *      BM_ETIMEDOUT, leaving the worker to abort the communicator (RCCL's
- *      bootstrap can block until every rank has connected).  From then on a search ends with
+ *      BM_ETIMEDOUT.  RCCL's bootstrap can block inside that init until
+ *      every rank has connected (RCCL 2.27 does), so the worker may stay
+ *      there: the context keeps it as its pending join, aborts whatever
+ *      communicator it ends up with, and starts no second one -- a later
+ *      bm_ctx_join_rank() first waits up to its own timeout_ms for the
+ *      pending one to end and returns BM_ETIMEDOUT if it has not.
+ *      bm_ctx_destroy() leaves a still-blocked worker detached (it holds no
+ *      reference to the context); it ends with the process.  The context
+ *      itself stays usable for searches of its own piece throughout.
+ *      From then on a search ends with
  *      one RCCL allgather of 32-byte slots {hash, nonce, status, 0}, so
  *      every rank returns the whole range's answer -- or, when any rank
  *      failed the call before the combine (it still takes part, with its
- *      status in the slot), every rank fails it together: the failing rank
- *      with its own status, the others with BM_EPEER.
+ *      status in the slot -- a HIP error while staging that slot included),
+ *      every rank fails it together: the failing rank with its own status,
+ *      the others with BM_EPEER.  Only a rank that cannot post its slot at
+ *      all aborts its communicator instead; its peers then see that as a
+ *      communicator error or wait for their peer timeout.
  * bm_ctx_create_rank() is both steps in one call (blocking join).
  * bm_ctx_set_peer_timeout(): a joined rank waits at most this long for the
  *   group's allgather after its own work ends (0, the default: no limit);
  *   past it the communicator is aborted and the call returns BM_ETIMEDOUT,
  *   as does every later search until bm_ctx_leave_rank().
  * bm_ctx_leave_rank(): drop the communicator; searches return the rank's
- *   own partial again.  bm_ctx_rank_joined(): 1 inside a group, else 0. */
+ *   own partial again.  bm_ctx_rank_joined(): 1 inside a group, else 0.
+ * bm_ctx_destroy() (any context) waits for its own streams, then drops every
+ *   communicator it holds with ncclCommAbort: teardown never waits on a peer,
+ *   even one that has died. */
 #define BM_RCCL_ID_BYTES 128
 int bm_rccl_unique_id(uint8_t* id /* BM_RCCL_ID_BYTES */);
 int bm_ctx_create_rank_local(int device, int rank, int world, bm_ctx_t** out);
@@ -179,11 +193,20 @@ typedef struct bm_stats {
     int32_t combine_used;  /* BM_COMBINED_*: how the partials were combined */
     int32_t rccl_status;   /* the RCCL failure this context fell back from or
                               stopped on (BM_ERCCL / BM_ETIMEDOUT), 0 if none */
-    uint32_t devices;      /* entries of dev_nonces / dev_span_ms */
+    uint32_t devices;      /* entries of dev_nonces / dev_span_ms / dev_rccl_* */
     uint32_t reserved;
     uint64_t dev_nonces[BM_MAX_STAT_DEVICES];  /* nonces each device of the context scanned */
     double dev_span_ms[BM_MAX_STAT_DEVICES];   /* each device's first operation to the end of
                                                   its reduction (timing on) */
+    /* What RCCL itself reports about the communicator the last call's
+     * combine ran over (combine_used = BM_COMBINED_RCCL; otherwise 0 / -1),
+     * so a multi-GPU measurement can show that the collective really spanned
+     * N ranks on N devices: */
+    int32_t rccl_nranks;   /* ncclCommCount: ranks in the communicator */
+    int32_t rccl_rank;     /* ncclCommUserRank of this process's (first) device */
+    int32_t dev_rccl_rank[BM_MAX_STAT_DEVICES];   /* ncclCommUserRank of each device of the context */
+    int32_t dev_rccl_device[BM_MAX_STAT_DEVICES]; /* ncclCommCuDevice: the HIP device RCCL runs that
+                                                     rank on */
     bm_launch_stat_t launch[BM_MAX_LAUNCH_STATS];
 } bm_stats_t;
 

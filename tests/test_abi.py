@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     lib = _lib.load()
-    assert lib.bm_abi_version() == _lib.BM_ABI_VERSION == 5
+    assert lib.bm_abi_version() == _lib.BM_ABI_VERSION == 6
     for code in range(0, -9, -1):
         assert lib.bm_strerror(code).decode() != "unknown status"
     assert lib.bm_strerror(-99).decode() == "unknown status"
@@ -118,31 +118,115 @@ def test_library_loads_with_immediate_binding():
     assert "RTLD_NOW" in inspect.getsource(_lib._open)
 
 
-def _c_client():
-    """examples/bm_c_client: a plain C program using only include/btcminer.h
-    (built by __graft_entry__.build(); rebuilt here if absent)."""
+GO_SHIM = os.path.join(ROOT, "go", "bitcoin", "miner", "gpu.go")
+C_PROXY = os.path.join(ROOT, "examples", "bm_c_client.c")
+
+
+def cgo_preamble():
+    """(C lines, {"CFLAGS": [...], "LDFLAGS": [...]}) of gpu.go's cgo preamble:
+    the comment right above `import "C"`."""
+    src = open(GO_SHIM).read()
+    m = re.search(r"/\*\n(.*?)\*/\nimport \"C\"", src, flags=re.S)
+    assert m, "no cgo preamble in gpu.go"
+    lines, flags = [], {"CFLAGS": [], "LDFLAGS": []}
+    for ln in m.group(1).splitlines():
+        f = re.match(r"#cgo (CFLAGS|LDFLAGS): (.*)$", ln)
+        if f:
+            flags[f.group(1)] += f.group(2).split()
+        elif ln.strip():
+            lines.append(ln)
+    return lines, flags
+
+
+def go_calls(src, lang):
+    """Library functions in order of first call (bm_strerror aside: error paths)."""
+    pat = r"\bC\.(bm_\w+)\(" if lang == "go" else r"\b(bm_\w+)\("
+    seen = []
+    for name in re.findall(pat, src):
+        if name not in seen and name != "bm_strerror":
+            seen.append(name)
+    return seen
+
+
+def test_cgo_shim_and_c_proxy_agree():
+    """the cgo shim is a file (go/bitcoin/miner/gpu.go, build tag
+    gpu, with its non-gpu twin and the miner.go patch), and the C proxy makes
+    the same calls under the same preamble: its preamble block is gpu.go's
+    C text line for line, and its calls into the library come in gpu.go's
+    order (create, num_devices, set_balance, search, destroy)."""
+    src = open(GO_SHIM).read()
+    assert src.startswith("//go:build gpu\n") and "package main" in src and "func scan(" in src
+    assert "unsafe.Pointer(nil)" not in src  # no placeholder to silence an unused import
+    cpu = open(os.path.join(ROOT, "go", "bitcoin", "miner", "scan_cpu.go")).read()
+    assert cpu.startswith("//go:build !gpu\n") and "func scan(data string, lower, upper uint64)" in cpu
+    lines, flags = cgo_preamble()
+    proxy = open(C_PROXY).read()
+    block = proxy.split("/* ---- cgo preamble of go/bitcoin/miner/gpu.go (verbatim) ---- */\n")[1]
+    block = block.split("/* ---- end of the cgo preamble ---- */")[0]
+    assert block.splitlines() == lines, (block, lines)
+    assert any(f.startswith("-I") for f in flags["CFLAGS"]) and "-lbtcminer" in flags["LDFLAGS"]
+    main = proxy.split("int main(")[1]
+    want = go_calls(src, "go")
+    assert want == ["bm_ctx_create", "bm_ctx_num_devices", "bm_ctx_set_balance", "bm_search_gpu",
+                    "bm_ctx_destroy"], want
+    got = [c for c in go_calls(main, "c") if c not in ("bm_abi_version", "bm_hash_gpu")]
+    assert got == want, got
+
+
+def test_miner_patch_applies_to_the_reference():
+    """go/bitcoin/miner/miner_go.patch replaces exactly miner.go:58-65 (the
+    per-nonce loop) with the scan() call and keeps the Result write; checked
+    with `patch` on a scratch copy of the reference file (this container only;
+    the GPU box has no /root/reference)."""
+    import shutil
     import subprocess
-    exe = os.path.join(ROOT, "examples", "bm_c_client")
-    deps = [os.path.join(ROOT, "examples", "bm_c_client.c"), os.path.join(ROOT, "include", "btcminer.h")]
-    if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(d) for d in deps):
-        subprocess.check_call(["gcc", "-O2", "-I", os.path.join(ROOT, "include"),
-                               os.path.join(ROOT, "examples", "bm_c_client.c"),
-                               "-L", os.path.join(ROOT, "distributed_bitcoin_minter_amd"), "-lbtcminer",
-                               "-Wl,-rpath,$ORIGIN/../distributed_bitcoin_minter_amd", "-o", exe])
+    import tempfile
+    ref = "/root/reference/project2/bitcoin/miner/miner.go"
+    if not os.path.exists(ref):
+        pytest.skip("reference tree absent")
+    with tempfile.TemporaryDirectory() as d:
+        os.makedirs(os.path.join(d, "bitcoin", "miner"))
+        shutil.copy(ref, os.path.join(d, "bitcoin", "miner", "miner.go"))
+        patch = os.path.join(ROOT, "go", "bitcoin", "miner", "miner_go.patch")
+        subprocess.run(["patch", "-p1", "-s", "-i", patch], cwd=d, check=True, capture_output=True)
+        got = open(os.path.join(d, "bitcoin", "miner", "miner.go")).read()
+    assert "bitcoin.Hash(" not in got.split("func workWorkWorkWorkWork")[1].split("\n}\n")[0]
+    assert "min_hash, min_nonce, scan_err := scan(job_msg.Data, job_msg.Lower, job_msg.Upper)" in got
+    assert "result := bitcoin.NewResult(min_hash, min_nonce)" in got
+
+
+def _c_client(tmp):
+    """Build examples/bm_c_client.c the way cgo would build gpu.go: with the
+    preamble's own #cgo CFLAGS / LDFLAGS, ${SRCDIR} being the file's place in
+    a reference checkout (project2/bitcoin/miner) with this repository as
+    btcminer/ next to project2/ (gpu.go's header)."""
+    import subprocess
+    srcdir = os.path.join(tmp, "project2", "bitcoin", "miner")
+    os.makedirs(srcdir)
+    os.symlink(ROOT, os.path.join(tmp, "btcminer"))
+    _, flags = cgo_preamble()
+    sub = [f.replace("${SRCDIR}", srcdir) for f in flags["CFLAGS"]]
+    ld = [f.replace("${SRCDIR}", srcdir) for f in flags["LDFLAGS"]]
+    exe = os.path.join(tmp, "bm_c_client")
+    subprocess.check_call(["gcc", "-O2", "-Wall", "-Werror", *sub, C_PROXY, *ld, "-o", exe])
     return exe
 
 
 @pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")
-def test_c_consumer_links_and_fails_loudly_without_gpu():
+def test_c_consumer_links_and_fails_loudly_without_gpu(tmp_path):
     import subprocess
-    r = subprocess.run([_c_client(), "bradfitz", "0", "9999"], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([_c_client(str(tmp_path)), "bradfitz", "0", "9999"], capture_output=True, text=True,
+                       timeout=60)
     assert r.returncode == 2 and r.stdout == "error -2 no usable gfx950 device\n"
 
 
 @pytest.mark.gpu
-def test_c_consumer_on_gpu():
+def test_c_consumer_on_gpu(tmp_path):
     import subprocess
-    r = subprocess.run([_c_client(), "bradfitz", "0", "9999"], capture_output=True, text=True, timeout=60)
+    exe = _c_client(str(tmp_path))
+    r = subprocess.run([exe, "bradfitz", "0", "9999"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and r.stdout == "Result 1419516646206828 9898\n", r.stdout + r.stderr
-    r = subprocess.run([_c_client(), "msg", "5", "4"], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([exe, "msg", "5", "4"], capture_output=True, text=True, timeout=60)
     assert r.stdout == "Result 18446744073709551615 18446744073709551615\n"  # empty range, miner.go:45-46
+    r = subprocess.run([exe, "", "0", "2"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.startswith("Result "), r.stdout + r.stderr  # empty msg: no copy

@@ -110,20 +110,35 @@ class FakeCtx:
     def close(self): pass
     def search(self, msg, lo, hi):
         piece = rank_piece(lo, hi, self.rank_, self.world_, self.shares)
+        self.piece = piece
         part = oracle.search(msg, *piece) if piece else (U64, U64)
         if self._joined:   # the in-library allgather: stand in with the whole range
             return oracle.search(msg, lo, hi)
         return part
+    def last_stats(self):  # bm_stats_t as the library fills it (ABI 6: RCCL's view of the communicator)
+        n = self.piece[1] - self.piece[0] + 1 if self.piece else 0
+        j = self._joined
+        return types.SimpleNamespace(
+            nonces=n, span_ms=1.0, combine_used=_lib.BM_COMBINED_RCCL if j else _lib.BM_COMBINED_LOCAL,
+            rccl_status=0, rccl_nranks=self.world_ if j else 0, rccl_rank=self.rank_ if j else -1, devices=1,
+            dev_nonces=[n], dev_span_ms=[1.0], dev_rccl_rank=[self.rank_ if j else -1],
+            dev_rccl_device=[0 if j else -1])
 
 bench.Context = FakeCtx
 bench.device_count = lambda: 1
 bench.rccl_unique_id = lambda: os.urandom(128)
+# every rank sees one device (a visibility mask), device 0 -- on its own GPU
+bench.device_pci_bus_id = lambda d: "0000:%02x:00.0" % (0x10 + int(os.environ.get("FAKE_BUS", os.environ["RANK"])))
 args = types.SimpleNamespace(rehearse_one_gpu=False, combine=os.environ.get("COMBINE", "rccl"))
-ctx, grp, search, how, dev = bench.open_contexts(args, int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"]),
-                                                 int(os.environ["LOCAL_RANK"]))
+world = int(os.environ["WORLD_SIZE"])
+ctx, grp, search, how, dev = bench.open_contexts(args, world, int(os.environ["RANK"]), int(os.environ["LOCAL_RANK"]))
 res = search(b"bradfitz", 0, 99_999)
+# the line's per-rank summaries and its validity, as main() builds them
+slots = grp.gather(bench.rank_summary(grp.rank, dev, [bench.step_record(ctx.last_stats())], None))
+valid = bench.scaling_validity(world, slots, args.combine, False)
 grp.close()
-print(json.dumps({"rank": grp.rank, "how": how, "dev": dev, "joined": ctx.joined(), "res": list(res)}))
+print(json.dumps({"rank": grp.rank, "how": how, "dev": dev, "joined": ctx.joined(), "res": list(res),
+                  "slots": slots, "valid": valid}))
 """
 
 
@@ -154,6 +169,12 @@ def test_bench_ranks_join_together(oracle):
     assert len(res) == 3, [e[-2000:] for _, _, e in outs]
     assert all(r["joined"] and "RCCL allgather" in r["how"] and r["res"] == want for r in res)
     assert all(r["dev"] == 0 for r in res)  # one visible device per rank (a visibility mask): device 0
+    # the line shows what RCCL reported -- 3 ranks, numbered 0..2, on 3 distinct GPUs
+    for r in res:
+        assert [s["rccl_nranks"] for s in r["slots"]] == [3, 3, 3]
+        assert [s["rccl_rank"] for s in r["slots"]] == [0, 1, 2]
+        assert len({s["pci_bus_id"] for s in r["slots"]}) == 3
+        assert r["valid"] == {"scaling_valid": True}, r["valid"]
 
 
 def test_bench_ranks_fall_back_together_when_one_join_fails(oracle):
@@ -167,9 +188,19 @@ def test_bench_ranks_fall_back_together_when_one_join_fails(oracle):
     for r in res:
         assert not r["joined"] and r["res"] == want
         assert "rendezvous gather" in r["how"] and "RCCL group failed: rank 1" in r["how"], r["how"]
+        # --combine rccl that fell back: not a valid scaling line, and it says why
+        assert r["valid"]["scaling_valid"] is False
+        assert any("instead of one RCCL allgather" in w for w in r["valid"]["scaling_invalid"]), r["valid"]
+        assert all(s["rccl_nranks"] == 0 and s["combine"] == "local" for s in r["slots"])
     outs = _rank_setup(2, COMBINE="gather")
     res = [json.loads(o.strip().splitlines()[-1]) for rc, o, e in outs if rc == 0]
     assert len(res) == 2 and all("--combine gather" in r["how"] and r["res"] == want for r in res)
+    assert all(r["valid"] == {"scaling_valid": True} for r in res)  # the combine the run asked for
+    # ranks that share one GPU (same PCI bus id): never a valid scaling line
+    outs = _rank_setup(2, COMBINE="gather", FAKE_BUS="0")
+    res = [json.loads(o.strip().splitlines()[-1]) for rc, o, e in outs if rc == 0]
+    assert len(res) == 2 and all(r["valid"]["scaling_valid"] is False for r in res)
+    assert all(any("1 distinct GPUs" in w for w in r["valid"]["scaling_invalid"]) for r in res)
 
 
 def test_bench_ranks_stop_together_when_one_context_fails():
@@ -191,3 +222,38 @@ def test_kernel_compressions_per_nonce():
     assert bench.kernel_compressions(L(nbv=1, pad_block=1, inner_digits=2)) == 2
     assert bench.kernel_compressions(L(nbv=2, pad_block=0, inner_digits=2)) == 1.01
     assert bench.kernel_compressions(L(nbv=2, pad_block=0, inner_digits=1)) == 1.1
+
+
+def test_scaling_validity_cases():
+    """bench.scaling_validity: an N > 1 line is valid only for N slots on N
+    distinct GPUs combined the way the run asked for; RCCL must itself report
+    N ranks numbered 0..N-1."""
+    def slot(i, bus=None, combine="rccl", nranks=4, rank=None):
+        return {"pci_bus_id": bus or f"0000:{i:02x}:00.0", "combine": combine, "rccl_nranks": nranks,
+                "rccl_rank": i if rank is None else rank}
+    ok = [slot(i) for i in range(4)]
+    assert bench.scaling_validity(4, ok, "rccl", False) == {"scaling_valid": True}
+    v = bench.scaling_validity(4, ok, "rccl", True)
+    assert v["scaling_valid"] is False and "rehearsal" in v["scaling_invalid"][0]
+    v = bench.scaling_validity(4, [slot(i, nranks=1, rank=0) for i in range(4)], "rccl", False)
+    assert not v["scaling_valid"] and any("of [1] ranks" in w for w in v["scaling_invalid"])
+    v = bench.scaling_validity(4, [slot(i, combine="host") for i in range(4)], "rccl", False)
+    assert not v["scaling_valid"] and "combine host" in v["scaling_invalid"][0]
+    v = bench.scaling_validity(4, ok[:3], "rccl", False)
+    assert not v["scaling_valid"]
+    v = bench.scaling_validity(2, [slot(0, bus="x", nranks=2), slot(1, bus="x", nranks=2)], "rccl", False)
+    assert not v["scaling_valid"] and "1 distinct GPUs" in v["scaling_invalid"][0]
+    assert bench.scaling_validity(2, [slot(i, combine="local") for i in range(2)], "gather", False)["scaling_valid"]
+
+
+def test_executed_roofline():
+    """roofline.executed: executed VALU lane-ops (PMC when committed, else the
+    static count) over the launch time, against 78.64 T and the live-clock
+    peak; C2's round-3 figures give about 0.885."""
+    e = bench.executed_roofline(2 ** 32, 2 ** 32 / 55.5e6, 1254.0, "p.json", 1250, 2.25)
+    assert e["valu_per_nonce"] == 1254.0 and "PMC" in e["src"]
+    assert abs(e["frac"] - 0.885) < 0.002
+    assert abs(e["frac_live_clock"] - e["frac"] * 2.4 / 2.25) < 1e-3
+    e = bench.executed_roofline(10 ** 9, 20.0, None, None, 1250, None)
+    assert e["valu_per_nonce"] == 1250 and "static" in e["src"] and "frac_live_clock" not in e
+    assert bench.executed_roofline(1, 1.0, None, None, None, 2.0) is None

@@ -80,5 +80,13 @@ def test_client_rejects_max_nonce_go_would_reject():
     2^64-1 (Python's int() alone would take spaces, a sign, underscores and
     other scripts' digits).  Leading zeros are fine, as in Go."""
     from distributed_bitcoin_minter_amd import client
-    for bad in ("-1", "18446744073709551616", "12x", "", " 5", "+5", "5_0", "0x10", "٥"):
+    for bad in ("-1", "18446744073709551616", "12x", "", " 5", "+5", "5_0", "0x10", "٥",
+                "9" * 21, "1" * 5000):  # ADVICE r3: past Python's 4300-digit int() limit too
         assert client.main(["127.0.0.1:1", "m", bad]) == 2, bad
+    # in range with leading zeros (Go's ParseUint takes them): past the usage check
+    import unittest.mock
+    with unittest.mock.patch.object(client, "request", return_value=(1, 2)) as req:
+        import io
+        buf = io.StringIO()
+        assert client.main(["127.0.0.1:1", "m", "0" * 4400 + "18446744073709551615"], out=buf) == 0
+        assert req.call_args[0][2] == 2 ** 64 - 1 and buf.getvalue() == "Result 1 2\n"

@@ -19,12 +19,13 @@
 #   prof_driver rocprofv3 kernel trace of the driver's exact bench command
 #   pmc         PMC passes (FETCH_SIZE, WRITE_SIZE, SQ) for C2 and C3, one counter group per run
 #   parity      tools/parity_campaign.py, PARITY_CASES (3,000) random cases, seed PARITY_SEED (303)
-#   lensweep    tools/len_sweep.py: GH/s for every message length 0..130 (every layout a 10-digit search hits)
+#   lensweep    tools/len_sweep.py: GH/s and the three roofline fractions for every message length 0..130
+#               (every layout a 10-digit search hits); lensweep_pmc: its SQ_INSTS_VALU pass
 #   ab          A/B of library variants: AB_LIBS="a.so b.so" (parity of each first, then alternating)
-# Logs and profiles land in gpurun_out/$TAG (TAG defaults to r03).
+# Logs and profiles land in gpurun_out/$TAG (TAG defaults to r04).
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 step() {  # name, seconds, command...
@@ -83,7 +84,12 @@ for phase in "$@"; do
           -- python3 tools/prof_one.py $C 2
       done ;;
     parity) step parity_campaign 600 python -u tools/parity_campaign.py ${PARITY_CASES:-3000} ${PARITY_SEED:-303} ;;
-    lensweep) step len_sweep 600 python -u tools/len_sweep.py 130 ;;
+    lensweep) step len_sweep 600 python -u tools/len_sweep.py --max-len 130 ;;
+    lensweep_pmc)
+      # one search per length under SQ_INSTS_VALU (one stream, no tail split:
+      # dispatch order = plan order); merge on the CPU with len_sweep.py --merge
+      step len_sweep_pmcpass 300 env BTCMINER_STREAMS=1 BTCMINER_TAIL=0 rocprofv3 --pmc SQ_INSTS_VALU \
+        -d "$OUT/pmc_lensweep" -o p --output-format csv -- python3 tools/len_sweep.py --pmc-pass --max-len 130 ;;
     ab)
       for lib in $AB_LIBS; do
         n=$(basename "$lib" .so)

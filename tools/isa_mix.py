@@ -7,7 +7,7 @@ every slow op takes an issue slot of its own, fast ops fill the second slot
 beside it.  Writes distributed_bitcoin_minter_amd/csrc/
 isa_mix.json, which bench.py reads to report the issue bound.
 
-    python tools/isa_mix.py 18:1 12:1 ...      (P:NBV pairs; default 18:1 12:1)
+    python tools/isa_mix.py 18:1 12:1 ...      (P:NBV pairs; default 18:1 12:1; "all": every layout)
 """
 import json
 import os
@@ -70,6 +70,8 @@ def asm_file(p, nbv):
 
 def main():
     pairs = sys.argv[1:] or ["18:1", "12:1"]
+    if pairs == ["all"]:  # every layout the library instantiates (bm_inst.hip)
+        pairs = [f"{p}:1" for p in range(64)] + [f"{p}:2" for p in range(19)]
     out = {"cycles_per_slot": CYC_SLOT, "model": "slots per 64 nonces = max(slow, (slow + fast) / 2)",
            "source": "tools/isa_mix.py on the built assembly (hipcc -O3 gfx950 + csrc/bm_prio.py)", "layouts": {}}
     for pr in pairs:
