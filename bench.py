@@ -143,10 +143,17 @@ def compressions_per_nonce(msg_len, digits):
     return -(-(msg_len + digits + 10) // 64) - (msg_len + 1) // 64
 
 
-def pmc_summary(config, p, nbv=1):
-    """The newest committed rocprofv3 PMC summary entry for search_kernel<p, nbv>
-    under this config (tools/pmc_summary.py: main launches only); PMC passes
-    cannot run inside this timed process."""
+def kernel_name(p, nbv, pad_block=0):
+    """Demangled name of the launch's kernel, as rocprof prints it (without
+    the argument list): search_kernel_padc for the folded padding-block
+    layouts (pad_block 2), search_kernel otherwise."""
+    return f"search_kernel_padc<{p}, 1>" if pad_block == 2 else f"search_kernel<{p}, {nbv}>"
+
+
+def pmc_summary(config, p, nbv=1, pad_block=0):
+    """The newest committed rocprofv3 PMC summary entry for the launch's
+    kernel under this config (tools/pmc_summary.py: main launches only); PMC
+    passes cannot run inside this timed process."""
     pats = [f"pmc_summary_{config}.json"] + (["pmc_summary.json"] if config == "C2" else [])
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary*.json")), reverse=True):
         if os.path.basename(path) not in pats:
@@ -156,7 +163,7 @@ def pmc_summary(config, p, nbv=1):
         except ValueError:
             continue
         for k, e in summ.items():
-            if f"search_kernel<{p}, {nbv}>" in k:
+            if kernel_name(p, nbv, pad_block) in k:
                 return e, os.path.relpath(path, ROOT)
     return None, None
 
@@ -166,7 +173,7 @@ def kernel_compressions(L):
     plus the constant padding block when the length does not fit (P >= 55);
     an NBV = 2 launch re-compresses the block before once per task of
     10^inner_digits nonces, not once per nonce (tools/len_sweep.py)."""
-    return 1 + L.pad_block + (L.nbv - 1) / 10 ** L.inner_digits
+    return 1 + (1 if L.pad_block else 0) + (L.nbv - 1) / 10 ** L.inner_digits
 
 
 def issue_bound(p, nbv, clock_ghz):
@@ -793,7 +800,8 @@ def main():
         c_eff = kernel_compressions(dom)  # blocks the kernel compresses per nonce
         c_survey = compressions_per_nonce(len(msg), dom.digits)
         achieved = dom.nonces * c_eff * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
-        pmc, pmc_src = pmc_summary(args.config, dom.p, dom.nbv)
+        kind = "c" if dom.pad_block == 2 else dom.nbv  # isa_mix.json key of the kernel
+        pmc, pmc_src = pmc_summary(args.config, dom.p, dom.nbv, dom.pad_block)
         pmc = pmc or {}
         cnt = pmc.get("counters", {})
         clock = pmc.get("clock_ghz")
@@ -810,7 +818,7 @@ def main():
                                 "(DESIGN.md §5, §8). FETCH_SIZE is not doubled: the guide's x2 is for 16-B/lane "
                                 "streaming reads, which this kernel does not issue",
                 "pmc_src": pmc_src,
-                "kernel": f"search_kernel<P={dom.p},NBV={dom.nbv}> ({dom.digits}-digit nonces)",
+                "kernel": f"{kernel_name(dom.p, dom.nbv, dom.pad_block)} ({dom.digits}-digit nonces)",
                 "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom.nonces,
                 "compressions_per_nonce": c_eff, "ops_per_nonce": c_eff * OPS_PER_COMPRESSION,
                 "grid": dom.grid, "tasks_per_thread": dom.tasks_per_thread, "inner_digits": dom.inner_digits}
@@ -850,7 +858,7 @@ def main():
             if box.get("cap_w"):
                 roof["power_cap_w"] = round(box["cap_w"], 1)
         ib_clock = live_clock or box.get("ghz_live") or box.get("ghz")
-        ib = issue_bound(dom.p, dom.nbv, ib_clock or clock or 0.0) if (ib_clock or clock) else None
+        ib = issue_bound(dom.p, kind, ib_clock or clock or 0.0) if (ib_clock or clock) else None
         if ib:
             if ib_clock:
                 where = (f"{box.get('searches')} untimed searches of the dominant kernel's range "
@@ -864,7 +872,7 @@ def main():
                 ib["note"] = "no clock measured on this box: the bound at the committed PMC clock, no frac"
             ib["role"] = "ceiling: the loop's own issue bound at the measured clock (DESIGN.md §5)"
             roof["issue_bound"] = ib
-        static = issue_bound(dom.p, dom.nbv, 1.0)  # the built loop's static VALU count
+        static = issue_bound(dom.p, kind, 1.0)  # the built loop's static VALU count
         roof["executed"] = executed_roofline(dom.nonces, dom_ms, roof.get("valu_per_nonce_pmc"), pmc_src,
                                              static and static["valu_per_nonce"], ib_clock)
         if calls:

@@ -29,8 +29,10 @@
 
 namespace bm {
 
-// search kernel table [nbv-1][P], filled by bm_inst.hip at load time
-static const void* g_search[2][64];
+// search kernel table [nbv-1][P], filled by bm_inst.hip at load time; row 2
+// holds search_kernel_padc<P> (P >= 55: a one-block message's padding-block
+// layouts with their constants folded)
+static const void* g_search[3][64];
 
 constexpr int kMaxInnerDigits = 2;  // S <= 100 nonces per task: small dequeue chunks, short tail
 constexpr uint32_t kNoncesPerLaneChunk = 100;  // default nonces per lane per dequeue (BTCMINER_CHUNK)
@@ -165,6 +167,7 @@ struct bm_ctx {
     uint64_t lane_chunk = bm::kNoncesPerLaneChunk;  // nonces per lane per dequeue, at most (BTCMINER_CHUNK)
     std::vector<uint32_t> shares;  // the partitioner's shares per slot (empty: near-equal pieces)
     bool balance = false;          // multi-device: shares follow each device's measured rate
+    bool padc = true;              // use search_kernel_padc where it applies (BTCMINER_PADC=0: never; A/B knob)
     // rank ctx: a join whose caller timed out while its worker was still
     // inside RCCL (the worker aborts the communicator if it ever gets one)
     std::shared_ptr<bm::JoinJob> pending_join;
@@ -173,7 +176,7 @@ struct bm_ctx {
 };
 
 extern "C" void bm_register_search_kernel(int p, int nbv, const void* fn) {
-    if (p >= 0 && p < 64 && (nbv == 1 || nbv == 2)) bm::g_search[nbv - 1][p] = fn;
+    if (p >= 0 && p < 64 && nbv >= 1 && nbv <= 3) bm::g_search[nbv - 1][p] = fn;
 }
 
 namespace bm {
@@ -192,8 +195,25 @@ int blocks_per_cu(bm_ctx* ctx, DeviceCtx& d, const void* fn) {
 // Size one launch: S = 10^ms nonces per task (ms <= digits of word LW),
 // chunks of 64*m tasks dequeued per wave, and at most one resident grid of
 // workgroups (any surplus workgroup simply finds the counter exhausted).
+// The PADC kernel applies when the segment's state before the varying block
+// is the IV and its padding block is the one of a one-block message ending
+// at byte P (bm_kernels.hpp pad_kw_const): the constants it folds.
+bool padc_applies(const bm_segment_t& s) {
+    if (!s.pad_block || s.nbv != 1 || s.p < 55) return false;
+    for (int q = 0; q < 8; ++q)
+        if (s.mid[q] != kIV256[q]) return false;
+    const KW64 kw = pad_kw_const(s.p);
+    uint32_t w[64];
+    for (int i = 0; i < 16; ++i) w[i] = s.pad_w[i];
+    host::expand(w);
+    for (int t = 0; t < 64; ++t)
+        if (kK256[t] + w[t] != kw.v[t]) return false;
+    return true;
+}
+
 int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_off, Launch& L) {
-    const void* fn = g_search[s.nbv - 1][s.p];
+    const bool padc = ctx->padc && padc_applies(s);
+    const void* fn = padc ? g_search[2][s.p] : g_search[s.nbv - 1][s.p];
     if (!fn) return BM_EINTERNAL;
     int ms = std::max(1, std::min(s.max_inner, kMaxInnerDigits));
     // word LW holds one digit: the kernel steps the next one in word LW-1
@@ -248,7 +268,7 @@ int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_
     std::memset(&L.stat, 0, sizeof L.stat);
     L.stat.p = s.p;
     L.stat.nbv = s.nbv;
-    L.stat.pad_block = s.pad_block;
+    L.stat.pad_block = padc ? 2 : s.pad_block;
     L.stat.digits = s.digits;
     L.stat.inner_digits = ms;
     L.stat.nonces = s.vhi - s.vlo + 1;
@@ -984,6 +1004,7 @@ void read_env(bm_ctx* ctx) {
         const unsigned long long v = std::strtoull(e, &end, 10);
         if (end != e && *end == '\0' && errno == 0 && v <= kMaxTailNonces) ctx->tail_nonces = v;
     }
+    if (const char* e = std::getenv("BTCMINER_PADC")) ctx->padc = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("BTCMINER_CHUNK")) {
         char* end = nullptr;
         errno = 0;

@@ -1,5 +1,6 @@
 // bm_inst.hip -- explicit instantiations of search_kernel<P, NBV> for
-// P in [BM_INST_PLO, BM_INST_PHI] and NBV = BM_INST_NBV, registered into the
+// P in [BM_INST_PLO, BM_INST_PHI] and NBV = BM_INST_NBV (and of
+// search_kernel_padc<P> for the padding-block P >= 55), registered into the
 // launcher's table at load time.  The Makefile compiles this file once per
 // P range (in parallel) so a full build of all 83 layouts stays short.
 #include "bm_kernels.hpp"
@@ -13,11 +14,17 @@ extern "C" void bm_register_search_kernel(int p, int nbv, const void* fn);
 #include <utility>
 
 namespace {
+// table slot nbv = 3: search_kernel_padc<P> (the padding-block layouts of a
+// one-block message, constants folded; NBV = 1 ranges only)
+template <int P>
+void register_one() {
+    bm_register_search_kernel(P, BM_INST_NBV, reinterpret_cast<const void*>(&bm::search_kernel<P, BM_INST_NBV>));
+    if constexpr (BM_INST_NBV == 1 && P >= 55)
+        bm_register_search_kernel(P, 3, reinterpret_cast<const void*>(&bm::search_kernel_padc<P>));
+}
 template <int... I>
 void register_all(std::integer_sequence<int, I...>) {
-    (bm_register_search_kernel(BM_INST_PLO + I, BM_INST_NBV,
-                               reinterpret_cast<const void*>(&bm::search_kernel<BM_INST_PLO + I, BM_INST_NBV>)),
-     ...);
+    (register_one<BM_INST_PLO + I>(), ...);
 }
 struct Registrar {
     Registrar() { register_all(std::make_integer_sequence<int, BM_INST_PHI - BM_INST_PLO + 1>{}); }

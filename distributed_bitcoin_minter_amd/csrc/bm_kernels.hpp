@@ -343,13 +343,16 @@ constexpr int kClockSlot = 16;
 #define BM_KATTR __attribute__((amdgpu_waves_per_eu(search_waves(P, NBV), 8)))
 #endif
 
-template <int P, int NBV>
-__global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
-    const SearchArgs A, Partial* __restrict__ part, unsigned long long* __restrict__ counter) {
+// PADC (the padding-block layouts of a one-block message): the IV and the
+// padding block's K + W are compile-time constants instead of kernargs
+// (kPadKW; the launcher checks the segment's mid / pad_w against them).
+template <int P, int NBV, bool PADC>
+BM_DEV void search_body(const SearchArgs& A, Partial* __restrict__ part, unsigned long long* __restrict__ counter) {
     static_assert(P >= 0 && P < 64 && (NBV == 1 || (NBV == 2 && P <= 18)), "layout");
     constexpr int LW = P / 4;                      // last-block word holding the last digit
     constexpr int BOFF = 16 * (NBV - 1);           // word offset of the last block
     constexpr bool PADB = (NBV == 1) && (P >= 55); // a constant padding block follows
+    static_assert(!PADC || PADB, "PADC is a padding-block layout");
     // Word LW holds only the last digit (P%4 == 0): a task's second digit is
     // stepped by an outer loop in word LW-1 (round LW-1 redone per step), so
     // tasks stay 100 nonces long instead of 10.
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
 
             uint32_t st[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) st[q] = A.mid[q];
+            for (int q = 0; q < 8; ++q) st[q] = PADC ? kIV256[q] : A.mid[q];
             if constexpr (NBV == 2) {
                 uint32_t wa[16];
 #pragma unroll
@@ -488,7 +491,12 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
                         for (int q = 0; q < 8; ++q) z[q] = y[q];
                         static_for<0, 64>([&](auto I) {
                             constexpr int tt2 = decltype(I)::value;
-                            sha_round_kw<tt2>(z, A.padkw[tt2]);
+                            if constexpr (PADC) {
+                                constexpr uint32_t kw = kPadKW<P>.v[tt2];
+                                sha_round_kw<tt2>(z, kw);
+                            } else {
+                                sha_round_kw<tt2>(z, A.padkw[tt2]);
+                            }
                         });
                         h0 = y[0] + z[0];
                         h1 = y[1] + z[1];
@@ -544,6 +552,22 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
     best_n = lbest_n[threadIdx.x];
 #endif
     if (block_min<kBlock>(best_h, best_n)) part[A.part_off + blockIdx.x] = Partial{best_h, best_n};
+}
+
+template <int P, int NBV>
+__global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
+    const SearchArgs A, Partial* __restrict__ part, unsigned long long* __restrict__ counter) {
+    search_body<P, NBV, false>(A, part, counter);
+}
+
+// The padding-block layouts (P >= 55) of a one-block message, with their
+// constants folded (search_body's PADC); NBV is 1 (a parameter only so the
+// occupancy attribute reads as for search_kernel).
+template <int P, int NBV = 1>
+__global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel_padc(
+    const SearchArgs A, Partial* __restrict__ part, unsigned long long* __restrict__ counter) {
+    static_assert(NBV == 1 && P >= 55, "padding-block layouts only");
+    search_body<P, 1, true>(A, part, counter);
 }
 
 }  // namespace bm

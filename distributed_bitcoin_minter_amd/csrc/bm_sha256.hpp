@@ -28,6 +28,33 @@ constexpr uint32_t kK256[64] = {
 constexpr uint32_t kIV256[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
 
+// K[t] + W[t] of the constant padding block that follows a ONE-block
+// message whose last byte is at P >= 55 (no prefix block, so the state
+// entering the varying block is the IV): W0 = 0x80000000 when P = 63 (the
+// 0x80 byte spilled over), W15 = the message length in bits, W1..W14 = 0,
+// W16..W63 expanded at compile time.  The PADC kernels (bm_kernels.hpp) use
+// these as literal operands: no kernarg SGPRs, so their adds stay in the
+// fast class; the launcher checks a segment against them at run time.
+struct KW64 {
+    uint32_t v[64];
+};
+constexpr uint32_t crotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+constexpr KW64 pad_kw_const(int P) {
+    uint32_t w[64] = {};
+    w[0] = P == 63 ? 0x80000000u : 0u;
+    w[15] = 8u * (uint32_t)(P + 1);
+    for (int t = 16; t < 64; ++t) {
+        const uint32_t x = w[t - 15], y = w[t - 2];
+        w[t] = (crotr(y, 17) ^ crotr(y, 19) ^ (y >> 10)) + w[t - 7] + (crotr(x, 7) ^ crotr(x, 18) ^ (x >> 3)) +
+               w[t - 16];
+    }
+    KW64 r{};
+    for (int t = 0; t < 64; ++t) r.v[t] = kK256[t] + w[t];
+    return r;
+}
+template <int P>
+inline constexpr KW64 kPadKW = pad_kw_const(P);
+
 namespace host {
 
 inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }

@@ -162,7 +162,8 @@ typedef struct bm_launch_stat {
     int32_t device;       /* index into the context's device list */
     int32_t p;            /* byte position of the last digit in its SHA block */
     int32_t nbv;          /* varying blocks per task (1 or 2) */
-    int32_t pad_block;    /* 1 when a constant padding block follows */
+    int32_t pad_block;    /* 1 when a constant padding block follows; 2: the same, run by the
+                             kernel with that block's constants folded in (a one-block message) */
     int32_t digits;       /* decimal digits of every nonce in the launch */
     int32_t inner_digits; /* digits iterated by each thread's inner loop */
     uint64_t nonces;      /* nonces the launch is responsible for */

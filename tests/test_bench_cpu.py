@@ -220,6 +220,7 @@ def test_kernel_compressions_per_nonce():
     from types import SimpleNamespace as L
     assert bench.kernel_compressions(L(nbv=1, pad_block=0, inner_digits=2)) == 1
     assert bench.kernel_compressions(L(nbv=1, pad_block=1, inner_digits=2)) == 2
+    assert bench.kernel_compressions(L(nbv=1, pad_block=2, inner_digits=2)) == 2  # search_kernel_padc
     assert bench.kernel_compressions(L(nbv=2, pad_block=0, inner_digits=2)) == 1.01
     assert bench.kernel_compressions(L(nbv=2, pad_block=0, inner_digits=1)) == 1.1
 

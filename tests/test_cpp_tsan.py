@@ -18,6 +18,7 @@ race (TSan prints "WARNING: ThreadSanitizer" and, with halt_on_error, exits
 import os
 import subprocess
 import threading
+import time
 
 import pytest
 
@@ -111,6 +112,10 @@ def test_echo_concurrent_clients_under_drops(tsan, tmp_path):
         for echoed, sent in got.values():
             assert echoed == sent  # in order, exactly once
         lspnet.ResetDropPercent()
+        # the server still drops 20% of what it reads: give its resends of the
+        # last echoes some epochs to be acked before the clients go, or a
+        # loaded host can leave one unacked and the server declares it lost
+        time.sleep(0.5)
         for c in clients:
             c.Close()
         assert srv.finish().splitlines()[-1] == "closed ok"

@@ -327,6 +327,75 @@ def test_rank_group_bootstrap_two_ranks_one_gpu():
     assert all(o["seen"] == [BM_ERCCL, BM_ERCCL] for o in outs), outs
 
 
+_RANK_EPEER = r"""
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+from distributed_bitcoin_minter_amd import _lib
+_lib.load()
+from distributed_bitcoin_minter_amd import BtcMinerError, Context, rccl_unique_id
+from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
+out = {}
+with Rendezvous(timeout_s=120) as rz:
+    uid = rz.broadcast_bytes(rccl_unique_id() if rz.rank == 0 else None)
+    with Context(devices=[rz.rank], rank=rz.rank, world=rz.world) as c:
+        c.join(uid, timeout_ms=60_000)
+        c.set_peer_timeout(60_000)
+        out["ok"] = list(c.search(b"bradfitz", 0, 9999))
+        st = c.last_stats()
+        out["nranks"], out["rrank"], out["rdev"] = st.rccl_nranks, st.rccl_rank, st.dev_rccl_device[0]
+        if rz.rank == 1:
+            c.set_test_fault(0)  # this rank fails before the combine
+        try:
+            c.search(b"bradfitz", 0, 9999)
+            out["fault"] = 0
+        except BtcMinerError as e:
+            out["fault"] = e.status
+        c.set_test_fault(-1)
+        out["after"] = list(c.search(b"bradfitz", 0, 9999))  # the group survived
+        rz.barrier()
+print(json.dumps(dict(out, rank=rz.rank)))
+"""
+
+
+def test_rank_group_epeer_two_gpus():
+    """on a box with two distinct GPUs, a 2-rank group whose rank 1
+    fails a search before the combine: rank 1 returns its own status
+    (BM_EINTERNAL), rank 0 BM_EPEER -- neither waits -- and the next search
+    answers on both.  RCCL reports 2 ranks, one per device.  (RCCL refuses
+    two ranks on one GPU, so on a one-GPU box this is skipped and the
+    world > 1 status path is unpinned: DESIGN.md §6.)"""
+    from distributed_bitcoin_minter_amd import device_count
+    from distributed_bitcoin_minter_amd._lib import BM_EPEER
+    if device_count() < 2:
+        pytest.skip("needs two GPUs")
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", _RANK_EPEER, ROOT], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=240)
+            assert p.returncode == 0, e[-3000:]
+            outs.append(json.loads(o.strip().splitlines()[-1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    outs.sort(key=lambda o: o["rank"])
+    want = [1419516646206828, 9898]
+    assert all(o["ok"] == want and o["after"] == want for o in outs), outs
+    assert [o["fault"] for o in outs] == [BM_EPEER, BM_EINTERNAL], outs
+    assert [(o["nranks"], o["rrank"], o["rdev"]) for o in outs] == [(2, 0, 0), (2, 1, 1)], outs
+
+
 def test_weighted_device_split_on_one_gpu(oracle):
     """The range partitioner with explicit shares (bm_ctx_set_split): three
     device slots on GPU 0 with shares 1:2:5 scan exactly the pieces

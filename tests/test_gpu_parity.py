@@ -127,6 +127,49 @@ def test_edges(gpu_ctx, oracle):
         assert gpu_ctx.search(msg, lo, lo + 1400) == oracle.search(msg, lo, lo + 1400), d
 
 
+@pytest.fixture(scope="module")
+def generic_pad_ctx():
+    """A context that never uses search_kernel_padc (BTCMINER_PADC=0, read at
+    creation): the generic padding-block kernel for every such layout."""
+    import os
+    from distributed_bitcoin_minter_amd import Context
+    old = os.environ.get("BTCMINER_PADC")
+    os.environ["BTCMINER_PADC"] = "0"
+    try:
+        ctx = Context(num_gpus=1)
+    finally:
+        if old is None:
+            del os.environ["BTCMINER_PADC"]
+        else:
+            os.environ["BTCMINER_PADC"] = old
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("P", range(55, 64))
+def test_padding_block_layouts_folded_and_generic(gpu_ctx, generic_pad_ctx, oracle, P):
+    """The padding-block layouts (last digit at byte P >= 55 of its block, so
+    SHA-256's length words spill into a block of their own), 10-digit
+    nonces, both task shapes: a one-block message runs search_kernel_padc (IV
+    and padding constants folded; stats pad_block = 2), the same message
+    under BTCMINER_PADC=0 and a two-block message (prefix midstate) run the
+    generic kernel (pad_block = 1); every answer equals the oracle's."""
+    lo = 10 ** 9 + 7_777_777
+    hi = lo + 20_000
+    one = bytes(97 + i % 26 for i in range(P - 10))        # L + 1 + 10 bytes end at byte P of block 0
+    two = bytes(65 + i % 26 for i in range(P - 10 + 64))   # ... of block 1
+    for ctx, msg, pad in ((gpu_ctx, one, 2), (generic_pad_ctx, one, 1), (gpu_ctx, two, 1)):
+        want = oracle.search(msg, lo, hi, threads=8)
+        for td in (0, 2):
+            ctx.set_task_digits(td)
+            try:
+                assert ctx.search(msg, lo, hi) == want, (len(msg), pad, td)
+            finally:
+                ctx.set_task_digits(0)
+            st = ctx.last_stats()
+            assert [(st.launch[i].p, st.launch[i].pad_block) for i in range(st.recorded)] == [(P, pad)]
+
+
 def test_split_and_merge_equals_whole(gpu_ctx):
     """Size-independent property at full C2 size: scanning two halves and
     taking the lexicographic min equals one scan of the whole range."""

@@ -21,6 +21,8 @@
 #   parity      tools/parity_campaign.py, PARITY_CASES (3,000) random cases, seed PARITY_SEED (303)
 #   lensweep    tools/len_sweep.py: GH/s and the three roofline fractions for every message length 0..130
 #               (every layout a 10-digit search hits); lensweep_pmc: its SQ_INSTS_VALU pass
+#   ab_padc     A/B of search_kernel_padc against the generic padding-block kernel (L = 45..53)
+#   parity_pad  the padding-block parity tests and every kernel layout
 #   ab          A/B of library variants: AB_LIBS="a.so b.so" (parity of each first, then alternating)
 # Logs and profiles land in gpurun_out/$TAG (TAG defaults to r04).
 cd "$(dirname "$0")/.." || exit 2
@@ -90,6 +92,8 @@ for phase in "$@"; do
       # dispatch order = plan order); merge on the CPU with len_sweep.py --merge
       step len_sweep_pmcpass 300 env BTCMINER_STREAMS=1 BTCMINER_TAIL=0 rocprofv3 --pmc SQ_INSTS_VALU \
         -d "$OUT/pmc_lensweep" -o p --output-format csv -- python3 tools/len_sweep.py --pmc-pass --max-len 130 ;;
+    ab_padc) step ab_padc 600 python -u tools/ab_padc.py ${AB_REPS:-5} ;;
+    parity_pad) step parity_pad 300 $PYTEST tests/test_gpu_parity.py -m gpu -k "padding_block or every_kernel_layout" -q ;;
     ab)
       for lib in $AB_LIBS; do
         n=$(basename "$lib" .so)

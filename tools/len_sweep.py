@@ -77,14 +77,14 @@ def sweep(args):
                 pd = max(launches_of(probe.last_stats()), key=lambda x: x.nonces)
                 clock = pd.clock_ghz if pd.clock_ghz > 0 else None
             dom_ghs = dn / dms / 1e6 if dms > 0 else None
-            c = 1 + pad + (nbv - 1) / 10 ** ms  # NBV = 2: the block before once per task
+            c = 1 + (1 if pad else 0) + (nbv - 1) / 10 ** ms  # NBV = 2: the block before once per task
             line = {"len": L, "P": p, "nbv": nbv, "pad": pad, "launches": nl, "inner_digits": ms,
                     "GHs": round(n / wall / 1e6, 3), "dom_GHs": round(dom_ghs, 3) if dom_ghs else None,
                     "compressions_per_nonce": c}
             if dom_ghs:
                 line["canonical_frac"] = round(dom_ghs * 1e9 * c * bench.OPS_PER_COMPRESSION / 1e12 /
                                                bench.VALU_PEAK_T, 4)
-                ib = bench.issue_bound(p, nbv, clock or 1.0)
+                ib = bench.issue_bound(p, "c" if pad == 2 else nbv, clock or 1.0)
                 if ib:
                     line["valu_static"] = ib["valu_per_nonce"]
                     line["executed_frac"] = round(dom_ghs * 1e9 * ib["valu_per_nonce"] / 1e12 / bench.VALU_PEAK_T, 4)
@@ -108,7 +108,8 @@ def pmc_pass(args):
         for L in range(args.max_len + 1):
             ctx.search(message(L), LO, LO + args.nonces - 1)
             st = ctx.last_stats()
-            print(json.dumps({"len": L, "launches": [[x.p, x.nbv, x.nonces] for x in launches_of(st)]}), flush=True)
+            print(json.dumps({"len": L, "launches": [[x.p, x.nbv, x.nonces, x.pad_block] for x in launches_of(st)]}),
+                  flush=True)
 
 
 def merge(sweep_path, pass_path, csv_path):
@@ -127,17 +128,19 @@ def merge(sweep_path, pass_path, csv_path):
     planned = [tuple(x) for ln in open(pass_path) if ln.startswith("{") for x in json.loads(ln)["launches"]]
     if len(planned) != len(disp):
         sys.exit(f"{len(disp)} search-kernel dispatches under PMC, {len(planned)} launches printed by the pass")
-    per = collections.defaultdict(lambda: [0.0, 0])  # (P, NBV) -> [VALU lane-ops, nonces]
-    for d, (p, nbv, nonces) in zip(disp, planned):
-        if f"search_kernel<{p}, {nbv}>" not in names[d]:
-            sys.exit(f"dispatch {d} is {names[d]}, the pass planned <{p}, {nbv}>")
-        per[(p, nbv)][0] += valu[d] * 64
-        per[(p, nbv)][1] += nonces
+    per = collections.defaultdict(lambda: [0.0, 0])  # (P, NBV or "c") -> [VALU lane-ops, nonces]
+    for d, (p, nbv, nonces, *pad) in zip(disp, planned):
+        kind = "c" if pad and pad[0] == 2 else nbv  # "c": search_kernel_padc<P>
+        name = f"search_kernel_padc<{p}, 1>" if kind == "c" else f"search_kernel<{p}, {nbv}>"
+        if name not in names[d]:
+            sys.exit(f"dispatch {d} is {names[d]}, the pass planned {name}")
+        per[(p, kind)][0] += valu[d] * 64
+        per[(p, kind)][1] += nonces
     for ln in open(sweep_path):
         if not ln.startswith("{"):
             continue
         line = json.loads(ln)
-        v = per.get((line["P"], line["nbv"]))
+        v = per.get((line["P"], "c" if line.get("pad") == 2 else line["nbv"]))
         if v and v[1] and line.get("dom_GHs"):
             line["valu_pmc"] = round(v[0] / v[1], 1)
             line["executed_frac_pmc"] = round(line["dom_GHs"] * 1e9 * line["valu_pmc"] / 1e12 / bench.VALU_PEAK_T, 4)
