@@ -8,6 +8,10 @@ byte P >= 55 of block 0 (L = 45..53), REPS alternating searches of
 launch's rate for each and their ratio, and checks the two answers agree.
 
     python tools/ab_padc.py [reps] [nonces]        (defaults 5, 2^31)
+
+AB_LIBS="name=path.so ..." adds one more search_kernel_padc context per
+library build (e.g. a build with another bm_prio.py option), alternating
+with the two above; ratios are against the generic kernel.
 """
 import json
 import os
@@ -29,35 +33,39 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 31
     lo = 10 ** 9
     os.environ["BTCMINER_PADC"] = "0"
-    generic = Context(devices=[0])
+    ctxs = [("generic", Context(devices=[0]))]
     del os.environ["BTCMINER_PADC"]
-    folded = Context(devices=[0])
-    for c in (generic, folded):
+    ctxs.append(("padc", Context(devices=[0])))
+    for spec in os.environ.get("AB_LIBS", "").split():
+        name, path = spec.split("=", 1)
+        ctxs.append((name, Context(devices=[0], lib_path=os.path.abspath(path))))
+    for _, c in ctxs:
         c.set_timing(True)
-    summary = []
+    summary = {name: [] for name, _ in ctxs[1:]}
     for L in range(45, 54):
         msg = bytes(97 + (i % 26) for i in range(L))
-        ans = {}
-        rates = {"padc": [], "generic": []}
-        for name, c in (("padc", folded), ("generic", generic)):
-            ans[name] = c.search(msg, lo, lo + n - 1)  # warm
+        ans = {name: c.search(msg, lo, lo + n - 1) for name, c in ctxs}  # warm
+        rates = {name: [] for name, _ in ctxs}
         for _ in range(reps):
-            for name, c in (("padc", folded), ("generic", generic)):
+            for name, c in ctxs:
                 assert c.search(msg, lo, lo + n - 1) == ans[name]
                 r, pad = dom_rate(c)
-                assert pad == (2 if name == "padc" else 1), (name, pad)
+                assert pad == (1 if name == "generic" else 2), (name, pad)
                 rates[name].append(r)
-        assert ans["padc"] == ans["generic"], (L, ans)
-        a = sum(rates["padc"]) / reps
-        b = sum(rates["generic"]) / reps
-        line = {"len": L, "P": L + 10, "padc_GHs": round(a, 3), "generic_GHs": round(b, 3),
-                "ratio": round(a / b, 4), "padc_runs": [round(x, 2) for x in rates["padc"]],
-                "generic_runs": [round(x, 2) for x in rates["generic"]], "answer": list(ans["padc"])}
-        summary.append(line["ratio"])
+        assert len(set(ans.values())) == 1, (L, ans)
+        base = sum(rates["generic"]) / reps
+        line = {"len": L, "P": L + 10, "answer": list(ans["generic"])}
+        for name, _ in ctxs:
+            m = sum(rates[name]) / reps
+            line[f"{name}_GHs"] = round(m, 3)
+            line[f"{name}_runs"] = [round(x, 2) for x in rates[name]]
+            if name != "generic":
+                line[f"{name}_ratio"] = round(m / base, 4)
+                summary[name].append(m / base)
         print(json.dumps(line), flush=True)
-    print(json.dumps({"mean_ratio": round(sum(summary) / len(summary), 4)}), flush=True)
-    generic.close()
-    folded.close()
+    print(json.dumps({f"{k}_mean_ratio": round(sum(v) / len(v), 4) for k, v in summary.items()}), flush=True)
+    for _, c in ctxs:
+        c.close()
 
 
 if __name__ == "__main__":
