@@ -828,7 +828,11 @@ def main():
             roof["survey_compressions_per_nonce"] = c_survey
             roof["survey_frac"] = round(dom.nonces * c_survey * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
                                         / VALU_PEAK_T, 4)
-        if "SQ_INSTS_VALU" in cnt:  # wave-instructions: x64 lanes
+        if pmc.get("valu_per_nonce"):  # SQ_INSTS_VALU x 64 lanes / the profiled launch's nonces
+            roof["valu_per_nonce_pmc"] = round(pmc["valu_per_nonce"], 1)
+        elif "SQ_INSTS_VALU" in cnt and n == 1 and world == 1:
+            # an older summary without the profiled launch's nonces: the PMC pass
+            # ran this config's N = 1 call, whose dominant launch is this one
             roof["valu_per_nonce_pmc"] = round(cnt["SQ_INSTS_VALU"] * 64 / dom.nonces, 1)
         if "SQ_ACTIVE_INST_VALU2" in cnt and cnt.get("SQ_INSTS_VALU"):
             roof["valu_dual_issued_frac_pmc"] = round(cnt["SQ_ACTIVE_INST_VALU2"] / cnt["SQ_INSTS_VALU"], 4)

@@ -81,7 +81,9 @@ int bm_device_pci_bus_id(int device, char* buf, int len);
  * never depend on it): BTCMINER_STREAMS = launch streams per device (1..4,
  * default 2); BTCMINER_TAIL = nonces split off the biggest launch into a
  * short-task launch of their own (default 16777216, 0 = off); BTCMINER_CHUNK =
- * nonces per lane per work-counter dequeue, at most (10..100000, default 100). */
+ * nonces per lane per work-counter dequeue, at most (10..100000, default 100);
+ * BTCMINER_PADC=0 = never use the padding-block kernel with folded constants
+ * (search_kernel_padc; default: wherever it applies). */
 int bm_ctx_create(int num_gpus, bm_ctx_t** out);
 /* Context over an explicit device list (e.g. {LOCAL_RANK} for one process
  * per GPU).  A device listed twice is allowed (a one-GPU rehearsal of the

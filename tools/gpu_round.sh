@@ -81,9 +81,9 @@ for phase in "$@"; do
           -- python3 tools/prof_one.py $C 2
         step pmc_${C}_write 90 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_${C}_write" -o w --output-format csv \
           -- python3 tools/prof_one.py $C 2
-        step pmc_${C}_sq 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
-          SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE -d "$OUT/pmc_${C}_sq" -o s --output-format csv \
-          -- python3 tools/prof_one.py $C 2
+        step pmc_${C}_sq 90 env PROF_ONE_LAUNCHES="$OUT/pmc_${C}_launches.json" rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU \
+          SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE \
+          -d "$OUT/pmc_${C}_sq" -o s --output-format csv -- python3 tools/prof_one.py $C 2
       done ;;
     parity) step parity_campaign 600 python -u tools/parity_campaign.py ${PARITY_CASES:-3000} ${PARITY_SEED:-303} ;;
     lensweep) step len_sweep 600 python -u tools/len_sweep.py --max-len 130 ;;

@@ -7,7 +7,10 @@ effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration) and VALU issue rate.
 Usage: pmc_summary.py <out_dir> [gpurun_out] [config]
 With a config (C2, C3 ...) only the passes under <gpurun_out>/pmc_<config>_*
 are read and the summary is written as pmc_summary_<config>.json (what
-bench.py looks up for that config's roofline fields)."""
+bench.py looks up for that config's roofline fields).  With the call's
+launches (<gpurun_out>/pmc_<config>_launches.json, written by
+tools/prof_one.py under PROF_ONE_LAUNCHES) each kernel also gets
+valu_per_nonce = SQ_INSTS_VALU x 64 / the nonces of its main launch."""
 import collections
 import csv
 import glob
@@ -28,6 +31,15 @@ for f in glob.glob(os.path.join(src, f"pmc_{cfg}_*" if cfg else "pmc_*", "*_coun
         per[k][d][r["Counter_Name"]] = per[k][d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         dur[k][d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
 MIN_CLOCK_S = 0.005  # clock only from launches at least this long
+# the profiled call's launches (tools/prof_one.py, PROF_ONE_LAUNCHES): the
+# main launch of each kernel layout and its nonces, so SQ_INSTS_VALU becomes
+# VALU per nonce (size-independent; bench.py's executed roofline uses it)
+main_nonces = {}
+lj = os.path.join(src, f"pmc_{cfg}_launches.json") if cfg else None
+if lj and os.path.exists(lj):
+    for x in json.load(open(lj)):
+        name = f"search_kernel_padc<{x['p']}, 1>" if x["pad_block"] == 2 else f"search_kernel<{x['p']}, {x['nbv']}>"
+        main_nonces[name] = max(main_nonces.get(name, 0), x["nonces"])
 res = {}
 for k, disp in per.items():
     if "search_kernel" not in k:
@@ -46,6 +58,10 @@ for k, disp in per.items():
         acc["_dur_s"].append(dur[k][d])
     m = {c: sum(v) / len(v) for c, v in acc.items()}
     e = {"counters": {c: v for c, v in m.items() if not c.startswith("_")}, "duration_ms": m["_dur_s"] * 1e3}
+    for name, nn in main_nonces.items():
+        if name + "(" in k and "SQ_INSTS_VALU" in m:
+            e["nonces_per_launch"] = nn
+            e["valu_per_nonce"] = m["SQ_INSTS_VALU"] * 64 / nn
     if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
         e["hbm_bytes_per_launch"] = int((m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024)
     if "GRBM_GUI_ACTIVE" in m and m["_dur_s"] >= MIN_CLOCK_S:

@@ -11,4 +11,10 @@ with Context(devices=[0]) as ctx:
     for _ in range(reps):
         r = ctx.search(bytes.fromhex(c["msg_hex"]), c["lower"], c["upper"])
         assert r == (c["hash"], c["nonce"]), r
+    # PROF_ONE_LAUNCHES=path: the last call's launches (kernel layout, nonces),
+    # so tools/pmc_summary.py can turn a counter per dispatch into one per nonce
+    if os.environ.get("PROF_ONE_LAUNCHES"):
+        st = ctx.last_stats()
+        json.dump([{"p": x.p, "nbv": x.nbv, "pad_block": x.pad_block, "nonces": x.nonces}
+                   for x in (st.launch[i] for i in range(st.recorded))], open(os.environ["PROF_ONE_LAUNCHES"], "w"))
 print("ok", cfg, r)
