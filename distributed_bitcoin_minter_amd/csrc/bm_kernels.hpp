@@ -85,8 +85,23 @@ BM_DEV void sha_round(uint32_t (&s)[8], uint32_t w) {
     h = t1 + bsig0(a) + maj(a, b, c);
 }
 
-// Same round with K[T] + W[T] supplied pre-added (constant padding block).
-template <int T>
+#ifndef BM_PAD_ADD3S  // generic padding block: the K+W kernarg inside one v_add3 (A/B knob)
+#define BM_PAD_ADD3S 1
+#endif
+
+// a + s + b as ONE v_add3_u32 reading the wave-uniform s from its SGPR.
+// Written in C, LLVM adds s on its own first (v_add_u32 v, s, v: an SGPR
+// operand makes it a slow-class op), then v_add3 -- two slow ops where one
+// slow v_add3 plus one fast v_add_u32 of the third term does.
+BM_DEV uint32_t add3_sgpr(uint32_t a, uint32_t s, uint32_t b) {
+    uint32_t r;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(s), "v"(b));
+    return r;
+}
+
+// Same round with K[T] + W[T] supplied pre-added (constant padding block):
+// a compile-time literal (search_kernel_padc) or a kernarg SGPR.
+template <int T, bool KW_SGPR = false>
 BM_DEV void sha_round_kw(uint32_t (&s)[8], uint32_t kw) {
     uint32_t& a = s[(0 - T) & 7];
     uint32_t& b = s[(1 - T) & 7];
@@ -96,7 +111,11 @@ BM_DEV void sha_round_kw(uint32_t (&s)[8], uint32_t kw) {
     uint32_t& f = s[(5 - T) & 7];
     uint32_t& g = s[(6 - T) & 7];
     uint32_t& h = s[(7 - T) & 7];
-    const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw;
+    uint32_t t1;
+    if constexpr (KW_SGPR && BM_PAD_ADD3S)
+        t1 = add3_sgpr(h, kw, ch(e, f, g)) + bsig1(e);
+    else
+        t1 = h + bsig1(e) + ch(e, f, g) + kw;
     d += t1;
     h = t1 + bsig0(a) + maj(a, b, c);
 }
@@ -495,7 +514,7 @@ BM_DEV void search_body(const SearchArgs& A, Partial* __restrict__ part, unsigne
                                 constexpr uint32_t kw = kPadKW<P>.v[tt2];
                                 sha_round_kw<tt2>(z, kw);
                             } else {
-                                sha_round_kw<tt2>(z, A.padkw[tt2]);
+                                sha_round_kw<tt2, true>(z, A.padkw[tt2]);
                             }
                         });
                         h0 = y[0] + z[0];

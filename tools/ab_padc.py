@@ -9,9 +9,11 @@ launch's rate for each and their ratio, and checks the two answers agree.
 
     python tools/ab_padc.py [reps] [nonces]        (defaults 5, 2^31)
 
-AB_LIBS="name=path.so ..." adds one more search_kernel_padc context per
-library build (e.g. a build with another bm_prio.py option), alternating
-with the two above; ratios are against the generic kernel.
+AB_LIBS="name=path.so ..." adds one more context per library build (e.g. a
+build with another bm_prio.py option or kernel macro), alternating with the
+two above; ratios are against the generic kernel of the product library.
+AB_LENS="109-117" sweeps other message lengths (there: two-block messages,
+which every build runs with the generic padding-block kernel).
 """
 import json
 import os
@@ -42,19 +44,22 @@ def main():
     for _, c in ctxs:
         c.set_timing(True)
     summary = {name: [] for name, _ in ctxs[1:]}
-    for L in range(45, 54):
+    a, b = map(int, os.environ.get("AB_LENS", "45-53").split("-"))
+    for L in range(a, b + 1):
         msg = bytes(97 + (i % 26) for i in range(L))
         ans = {name: c.search(msg, lo, lo + n - 1) for name, c in ctxs}  # warm
         rates = {name: [] for name, _ in ctxs}
+        pads = {}
         for _ in range(reps):
             for name, c in ctxs:
                 assert c.search(msg, lo, lo + n - 1) == ans[name]
                 r, pad = dom_rate(c)
-                assert pad == (1 if name == "generic" else 2), (name, pad)
+                assert pad >= 1 and (name != "generic" or pad == 1), (name, pad)
+                pads[name] = pad
                 rates[name].append(r)
         assert len(set(ans.values())) == 1, (L, ans)
         base = sum(rates["generic"]) / reps
-        line = {"len": L, "P": L + 10, "answer": list(ans["generic"])}
+        line = {"len": L, "P": (L + 10) % 64, "pad_block": pads, "answer": list(ans["generic"])}
         for name, _ in ctxs:
             m = sum(rates[name]) / reps
             line[f"{name}_GHs"] = round(m, 3)
