@@ -13,7 +13,7 @@
 #   tests_multi tests/test_gpu_multi.py only
 #   bench       C2 bench line, 20 steps (the driver's N = 1 line); bench_c3, bench_c4: C3 / C4 on one GPU
 #   rehearse    the multi-GPU modes on one GPU: one process 2-way split, 2 torchrun ranks under a
-#               per-rank visibility mask, C4 over 8 one-process slots
+#               per-rank visibility mask, C4 over 8 one-process slots; rehearse8: 8 torchrun ranks on GPU 0
 #   c5          C5 at size: the native (C++) system and the Python one
 #   prof        rocprofv3 kernel traces of C2 (2 streams, 1 stream) and C3
 #   prof_driver rocprofv3 kernel trace of the driver's exact bench command
@@ -61,6 +61,10 @@ for phase in "$@"; do
       step rehearse2_mask 400 env HIP_VISIBLE_DEVICES=0 python -u -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 2
       step rehearse8_C4 300 $BENCH --config C4 --gpus 8 --rehearse-one-gpu --steps 1 --warmup 1 ;;
+    rehearse8)
+      # the driver's N = 8 launch, all 8 ranks masked onto GPU 0 (RCCL refuses: rendezvous gather)
+      step rehearse8_torchrun 400 env HIP_VISIBLE_DEVICES=0 python -u -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 --steps 2 --warmup 2 ;;
     c5)
       step c5_native 300 python -u tools/bench_c5_native.py
       step c5_python 300 python -u tools/bench_c5.py ;;
