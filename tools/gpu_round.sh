@@ -97,6 +97,11 @@ for phase in "$@"; do
       step len_sweep_pmcpass 300 env BTCMINER_STREAMS=1 BTCMINER_TAIL=0 rocprofv3 --pmc SQ_INSTS_VALU \
         -d "$OUT/pmc_lensweep" -o p --output-format csv -- python3 tools/len_sweep.py --pmc-pass --max-len 130 ;;
     ab_padc) step ab_padc 600 python -u tools/ab_padc.py ${AB_REPS:-5} ;;
+    structure)
+      # C2's 11 launches against one 10-digit range of the same size, live clock
+      step structure 300 python -u tools/ab_structure.py 8
+      step structure_1stream 300 env BTCMINER_STREAMS=1 python -u tools/ab_structure.py 8
+      step structure_notail 300 env BTCMINER_TAIL=0 python -u tools/ab_structure.py 8 ;;
     parity_pad) step parity_pad 300 $PYTEST tests/test_gpu_parity.py -m gpu -k "padding_block or every_kernel_layout" -q ;;
     ab)
       for lib in $AB_LIBS; do
