@@ -258,3 +258,26 @@ def test_executed_roofline():
     e = bench.executed_roofline(10 ** 9, 20.0, None, None, 1250, None)
     assert e["valu_per_nonce"] == 1250 and "static" in e["src"] and "frac_live_clock" not in e
     assert bench.executed_roofline(1, 1.0, None, None, None, 2.0) is None
+
+
+def test_one_process_device_summaries(monkeypatch):
+    """The one-process N-device line: each device slot carries its HIP device,
+    PCI bus id and its rank in the context's RCCL communicator (from the
+    stats' dev_rccl_*), and scaling_validity reads them: RCCL over 4 distinct
+    devices is valid; the host-copy fallback (no ranks) is not."""
+    from types import SimpleNamespace as NS
+    monkeypatch.setattr(bench, "device_pci_bus_id", lambda d: f"0000:{0x20 + d:02x}:00.0")
+
+    def stats(combine, nranks):
+        return NS(nonces=4 << 30, span_ms=80.0, combine_used=combine, rccl_status=0 if nranks else -4,
+                  rccl_nranks=nranks, rccl_rank=0 if nranks else -1, devices=4, dev_nonces=[1 << 30] * 4,
+                  dev_span_ms=[79.0, 80.0, 78.5, 79.5], dev_rccl_rank=list(range(4)) if nranks else [-1] * 4,
+                  dev_rccl_device=list(range(4)) if nranks else [-1] * 4)
+    from distributed_bitcoin_minter_amd import _lib
+    slots = bench.device_summaries([bench.step_record(stats(_lib.BM_COMBINED_RCCL, 4))], [0, 1, 2, 3])
+    assert [s["rccl_rank"] for s in slots] == [0, 1, 2, 3] and [s["rccl_device"] for s in slots] == [0, 1, 2, 3]
+    assert len({s["pci_bus_id"] for s in slots}) == 4 and all(s["combine"] == "rccl" for s in slots)
+    assert bench.scaling_validity(4, slots, "rccl", False) == {"scaling_valid": True}
+    slots = bench.device_summaries([bench.step_record(stats(_lib.BM_COMBINED_HOST, 0))], [0, 1, 2, 3])
+    v = bench.scaling_validity(4, slots, "rccl", False)
+    assert v["scaling_valid"] is False and "combine host" in v["scaling_invalid"][0]
