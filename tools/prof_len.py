@@ -21,5 +21,6 @@ with Context(devices=[0]) as ctx:
         launches += [{"len": L, "p": x.p, "nbv": x.nbv, "pad_block": x.pad_block, "nonces": x.nonces}
                      for x in (st.launch[i] for i in range(st.recorded))]
 if os.environ.get("PROF_ONE_LAUNCHES"):
-    json.dump(launches, open(os.environ["PROF_ONE_LAUNCHES"], "w"))
+    with open(os.environ["PROF_ONE_LAUNCHES"], "w") as f:
+        json.dump(launches, f)
 print("ok", sys.argv[1:])

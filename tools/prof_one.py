@@ -15,6 +15,7 @@ with Context(devices=[0]) as ctx:
     # so tools/pmc_summary.py can turn a counter per dispatch into one per nonce
     if os.environ.get("PROF_ONE_LAUNCHES"):
         st = ctx.last_stats()
-        json.dump([{"p": x.p, "nbv": x.nbv, "pad_block": x.pad_block, "nonces": x.nonces}
-                   for x in (st.launch[i] for i in range(st.recorded))], open(os.environ["PROF_ONE_LAUNCHES"], "w"))
+        with open(os.environ["PROF_ONE_LAUNCHES"], "w") as f:
+            json.dump([{"p": x.p, "nbv": x.nbv, "pad_block": x.pad_block, "nonces": x.nonces}
+                       for x in (st.launch[i] for i in range(st.recorded))], f)
 print("ok", cfg, r)
