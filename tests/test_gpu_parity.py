@@ -170,6 +170,28 @@ def test_padding_block_layouts_folded_and_generic(gpu_ctx, generic_pad_ctx, orac
             assert [(st.launch[i].p, st.launch[i].pad_block) for i in range(st.recorded)] == [(P, pad)]
 
 
+def _layout_ranges():
+    import json
+    import os
+    from conftest import ROOT
+    return json.load(open(os.path.join(ROOT, "tests", "golden", "layout_ranges.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", _layout_ranges(), ids=lambda c: f"L{c['len']}")
+def test_layout_full_range_goldens(gpu_ctx, case):
+    """Round 4's kernels at full size: a whole 2^32-nonce 10-digit range for
+    a padc message (L = 50, and L = 46 with the two-word inner loop), a
+    generic padding-block one after a prefix block (L = 114), and an NBV = 2
+    one (L = 59), against the AVX-512 oracle's full scans
+    (tests/golden/make_layout_golden.py); the launch stats name the kernel."""
+    msg = bytes.fromhex(case["msg_hex"])
+    assert gpu_ctx.search(msg, case["lower"], case["upper"]) == (case["hash"], case["nonce"])
+    st = gpu_ctx.last_stats()
+    dom = max((st.launch[i] for i in range(st.recorded)), key=lambda x: x.nonces)
+    want = {50: (1, 2), 46: (1, 2), 114: (1, 1), 59: (2, 0)}[case["len"]]
+    assert (dom.nbv, dom.pad_block) == want, (dom.nbv, dom.pad_block)
+
+
 def test_split_and_merge_equals_whole(gpu_ctx):
     """Size-independent property at full C2 size: scanning two halves and
     taking the lexicographic min equals one scan of the whole range."""
