@@ -890,6 +890,11 @@ def main():
             ach = sum(o for o, _ in calls) / len(calls) / (span * 1e-3) / 1e12
             roof["call"] = {"achieved": round(ach, 3), "frac": round(ach / VALU_PEAK_T, 4), "span_ms": round(span, 3),
                             "launches": ctx.last_stats().launches}
+            if ib and ib.get("frac") is not None and world == 1 and n == 1:
+                # this device's whole call (every launch, their common span)
+                # against the dominant loop's issue bound: the steadier figure
+                # (the dominant launch shares the GPU with the others)
+                roof["call"]["issue_frac"] = round(pers[-1]["nonces"] / span / 1e6 / ib["GHs_per_gpu"], 4)
         out["roofline"] = roof
     if world > 1 and any(c is not None for c in clocks):
         # each rank's GPU clock over the timed region (driver hwmon): what

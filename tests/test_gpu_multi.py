@@ -261,6 +261,8 @@ def test_bench_torchrun_rccl_world1():
     ex = out["roofline"]["executed"]  # executed VALU lane-ops, always below the peak
     assert ex and 0.5 < ex["frac"] < 1.0 and ex["valu_per_nonce"] > 1000, ex
     assert "ceiling" in out["roofline"]["issue_bound"]["role"]
+    call = out["roofline"]["call"]
+    assert "issue_frac" not in call or 0.8 < call["issue_frac"] < 1.05, call
 
 
 def test_split_range_matches_library(gpu_ctx):
