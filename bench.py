@@ -500,6 +500,23 @@ def calibrate_split(args, ctx, grp):
             "rates_nonces_per_ms": [round(r, 1) for r in rates]}
 
 
+def call_roofline(calls, launches, call_nonces, ib=None):
+    """roofline.call: the whole call on this device, every launch's
+    algorithmic ops (calls: (ops, span_ms) per timed step) over the span of
+    its launches.  Two streams overlap launches, which stretches each
+    launch's own event time (DESIGN.md §5).  With ib (the dominant loop's
+    issue bound, one device only), issue_frac = the call's nonces per second
+    over that bound: the steadier ceiling figure, since the dominant launch
+    shares the GPU with the call's other launches."""
+    span = sum(sp for _, sp in calls) / len(calls)
+    ach = sum(o for o, _ in calls) / len(calls) / (span * 1e-3) / 1e12
+    out = {"achieved": round(ach, 3), "frac": round(ach / VALU_PEAK_T, 4), "span_ms": round(span, 3),
+           "launches": launches}
+    if ib and ib.get("frac") is not None:
+        out["issue_frac"] = round(call_nonces / span / 1e6 / ib["GHs_per_gpu"], 4)
+    return out
+
+
 def _mean(xs):
     return sum(xs) / len(xs) if xs else 0.0
 
@@ -883,18 +900,8 @@ def main():
         roof["executed"] = executed_roofline(dom.nonces, dom_ms, roof.get("valu_per_nonce_pmc"), pmc_src,
                                              static and static["valu_per_nonce"], ib_clock)
         if calls:
-            # the whole call on this device: every launch's algorithmic ops over
-            # the span of its launches (two streams overlap launches, which
-            # stretches each launch's own event time)
-            span = sum(sp for _, sp in calls) / len(calls)
-            ach = sum(o for o, _ in calls) / len(calls) / (span * 1e-3) / 1e12
-            roof["call"] = {"achieved": round(ach, 3), "frac": round(ach / VALU_PEAK_T, 4), "span_ms": round(span, 3),
-                            "launches": ctx.last_stats().launches}
-            if ib and ib.get("frac") is not None and world == 1 and n == 1:
-                # this device's whole call (every launch, their common span)
-                # against the dominant loop's issue bound: the steadier figure
-                # (the dominant launch shares the GPU with the others)
-                roof["call"]["issue_frac"] = round(pers[-1]["nonces"] / span / 1e6 / ib["GHs_per_gpu"], 4)
+            roof["call"] = call_roofline(calls, ctx.last_stats().launches, pers[-1]["nonces"],
+                                         ib if world == 1 and n == 1 else None)
         out["roofline"] = roof
     if world > 1 and any(c is not None for c in clocks):
         # each rank's GPU clock over the timed region (driver hwmon): what

@@ -260,6 +260,19 @@ def test_executed_roofline():
     assert bench.executed_roofline(1, 1.0, None, None, None, 2.0) is None
 
 
+def test_call_roofline():
+    """roofline.call: the call's ops over its launches' span, and (one device)
+    its nonces per second against the dominant loop's issue bound; the
+    round-4 check run (profiles/r04/call_issue_frac.log) gives 0.971."""
+    ops = (2 ** 32) * bench.OPS_PER_COMPRESSION
+    c = bench.call_roofline([(ops, 80.6), (ops, 80.616)], 11, 2 ** 32, {"frac": 0.97, "GHs_per_gpu": 54.86})
+    assert c["launches"] == 11 and c["span_ms"] == 80.608
+    assert abs(c["achieved"] - 73.74) < 0.01 and abs(c["frac"] - c["achieved"] / bench.VALU_PEAK_T) < 1e-4
+    assert c["issue_frac"] == 0.9712
+    assert "issue_frac" not in bench.call_roofline([(ops, 80.6)], 11, 2 ** 32, None)
+    assert "issue_frac" not in bench.call_roofline([(ops, 80.6)], 11, 2 ** 32, {"GHs_per_gpu": 54.86, "frac": None})
+
+
 def test_one_process_device_summaries(monkeypatch):
     """The one-process N-device line: each device slot carries its HIP device,
     PCI bus id and its rank in the context's RCCL communicator (from the
