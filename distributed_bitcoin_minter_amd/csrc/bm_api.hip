@@ -163,7 +163,8 @@ struct bm_ctx {
     int group_status = 0;     // joined rank ctx whose communicator failed (BM_ERCCL / BM_ETIMEDOUT)
     int peer_timeout_ms = 0;  // joined rank ctx: wait at most this long for the group (0: no limit)
     int fault_after = -1;     // test hook: fail after enqueueing this many launches (-1: off)
-    int test_rccl_fault = 0;  // test hook: 1 communicator set-up fails, 2 every allgather fails
+    int test_rccl_fault = 0;  // test hook: 1 communicator set-up fails, 2 every allgather fails,
+                              // 3 the gathered slots report a failed peer (rank groups)
     uint64_t lane_chunk = bm::kNoncesPerLaneChunk;  // nonces per lane per dequeue, at most (BTCMINER_CHUNK)
     std::vector<uint32_t> shares;  // the partitioner's shares per slot (empty: near-equal pieces)
     bool balance = false;          // multi-device: shares follow each device's measured rate
@@ -700,6 +701,9 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
     st.combine_used = BM_COMBINED_RCCL;
     record_rccl(ctx, true);
     if (!copied) return own_rc != BM_OK ? own_rc : BM_EHIP;
+    // test hook: the last slot arrives carrying a peer's failure status, as
+    // a real peer's would (at world 1 that slot is this rank's own)
+    if (ctx->test_rccl_fault == 3) d.h_slots[world - 1].status = (uint64_t)(int64_t)BM_EHIP;
     for (int r = 0; r < world; ++r)
         if (d.h_slots[r].status != 0) return own_rc != BM_OK ? own_rc : BM_EPEER;
     if (own_rc != BM_OK) return own_rc;
@@ -1237,7 +1241,7 @@ int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches) {
 }
 
 int bm_ctx_set_test_rccl_fault(bm_ctx_t* ctx, int where) {
-    if (!ctx || where < 0 || where > 2) return BM_EINVAL;
+    if (!ctx || where < 0 || where > 3) return BM_EINVAL;
     ctx->test_rccl_fault = where;
     return BM_OK;
 }

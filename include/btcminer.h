@@ -299,7 +299,9 @@ int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches);
  * (ncclCommInitAll, or bm_ctx_join_rank), 2 = every allgather, before it is
  * enqueued.  A multi-device context then falls back to host copies; a
  * joined rank context fails the call (at world 1 only: a real group's peers
- * would wait for it until their peer timeout). */
+ * would wait for it until their peer timeout).  3 = a joined rank context's
+ * allgather succeeds but its last slot carries a failure status, as a failed
+ * peer's slot does: the call returns BM_EPEER and the group stays joined. */
 int bm_ctx_set_test_rccl_fault(bm_ctx_t* ctx, int where);
 
 /* ---- host-side plan introspection (pure CPU; used by the CPU tests) ---- */

@@ -59,6 +59,7 @@ def test_invalid_arguments_rejected():
     assert lib.bm_ctx_rank_joined(None, ctypes.byref(n)) == _lib.BM_EINVAL
     assert lib.bm_ctx_set_peer_timeout(None, 10) == _lib.BM_EINVAL
     assert lib.bm_ctx_set_test_rccl_fault(None, 1) == _lib.BM_EINVAL
+    assert lib.bm_ctx_set_test_rccl_fault(None, 3) == _lib.BM_EINVAL
     assert lib.bm_reduce_gpu(None, None, 0, ctypes.byref(r)) == _lib.BM_EINVAL
     assert lib.bm_ctx_set_test_fault(None, 0) == _lib.BM_EINVAL
     assert lib.bm_ctx_rank(None, ctypes.byref(n), ctypes.byref(n)) == _lib.BM_EINVAL

@@ -470,7 +470,7 @@ def test_bench_rehearsals_balance_after_warmup():
 # ---- fail-safe combines (ABI 5) ---------------------------------------------
 
 from distributed_bitcoin_minter_amd._lib import (BM_COMBINED_HOST, BM_COMBINED_LOCAL,  # noqa: E402
-                                                 BM_COMBINED_RCCL, BM_ERCCL, BM_ETIMEDOUT)
+                                                 BM_COMBINED_RCCL, BM_EPEER, BM_ERCCL, BM_ETIMEDOUT)
 
 
 @pytest.mark.parametrize("where", [1, 2])
@@ -545,7 +545,9 @@ def test_rank_contexts_outside_a_group(oracle):
 def test_rank_group_world1_status_and_leave(oracle):
     """A joined rank context (world 1 on this box) combines through the
     status-carrying allgather: a failure before the combine comes back as the
-    rank's own status; an allgather failure (test hook) aborts the
+    rank's own status; a gathered slot carrying a peer's failure (test hook
+    3) is BM_EPEER and leaves the group joined and usable; an allgather
+    failure (test hook 2) aborts the
     communicator and every later search returns BM_ERCCL until leave(); after
     leave() the context answers with its own partial; a fresh join works."""
     msg, lo, hi = b"bradfitz", 999_000_000, 1_000_999_999
@@ -564,6 +566,13 @@ def test_rank_group_world1_status_and_leave(oracle):
             assert ei.value.status == BM_EINTERNAL
         c.set_test_fault(-1)
         assert c.search(msg, lo, hi) == want                   # the group survived a rank-side failure
+        c.set_test_rccl_fault(3)
+        with pytest.raises(BtcMinerError) as ei:
+            c.search(msg, lo, hi)
+        assert ei.value.status == BM_EPEER and c.joined()
+        assert c.last_stats().combine_used == BM_COMBINED_RCCL
+        c.set_test_rccl_fault(0)
+        assert c.search(msg, lo, hi) == want                   # and a peer's reported failure
         c.set_test_rccl_fault(2)
         for _ in range(2):
             with pytest.raises(BtcMinerError) as ei:
