@@ -570,9 +570,9 @@ def test_rank_group_world1_status_and_leave(oracle):
         with pytest.raises(BtcMinerError) as ei:
             c.search(msg, lo, hi)
         assert ei.value.status == BM_EPEER and c.joined()
-        assert c.last_stats().combine_used == BM_COMBINED_RCCL
         c.set_test_rccl_fault(0)
         assert c.search(msg, lo, hi) == want                   # and a peer's reported failure
+        assert c.last_stats().combine_used == BM_COMBINED_RCCL  # over the same communicator
         c.set_test_rccl_fault(2)
         for _ in range(2):
             with pytest.raises(BtcMinerError) as ei:
