@@ -145,9 +145,24 @@ def compressions_per_nonce(msg_len, digits):
 
 def kernel_name(p, nbv, pad_block=0):
     """Demangled name of the launch's kernel, as rocprof prints it (without
-    the argument list): search_kernel_padc for the folded padding-block
-    layouts (pad_block 2), search_kernel otherwise."""
-    return f"search_kernel_padc<{p}, 1>" if pad_block == 2 else f"search_kernel<{p}, {nbv}>"
+    the argument list): the folded padding-block layouts are
+    search_kernel_padc<P, 1> (pad_block 2: a one-block message) and
+    search_kernel_padk<P, K, 1> (pad_block 2 + K: after K prefix blocks),
+    search_kernel<P, NBV> otherwise."""
+    if pad_block == 2:
+        return f"search_kernel_padc<{p}, 1>"
+    if pad_block > 2:
+        return f"search_kernel_padk<{p}, {pad_block - 2}, 1>"
+    return f"search_kernel<{p}, {nbv}>"
+
+
+def isa_key(p, nbv, pad_block=0):
+    """The launch's kernel in isa_mix.json: "P:NBV", "P:c" (padc), "P:kK" (padk)."""
+    if pad_block == 2:
+        return f"{p}:c"
+    if pad_block > 2:
+        return f"{p}:k{pad_block - 2}"
+    return f"{p}:{nbv}"
 
 
 def pmc_summary(config, p, nbv=1, pad_block=0):
@@ -176,7 +191,7 @@ def kernel_compressions(L):
     return 1 + (1 if L.pad_block else 0) + (L.nbv - 1) / 10 ** L.inner_digits
 
 
-def issue_bound(p, nbv, clock_ghz):
+def issue_bound(key, clock_ghz):
     """gfx950 VALU issue bound of the kernel's inner loop: each
     slow op (v_alignbit, v_add3, SGPR operand, ...) takes an issue slot of its
     own, fast ops of two waves share one, so a SIMD needs max(slow, (slow +
@@ -185,7 +200,7 @@ def issue_bound(p, nbv, clock_ghz):
     this kernel."""
     path = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc", "isa_mix.json")
     try:
-        lay = json.load(open(path))["layouts"][f"{p}:{nbv}"]
+        lay = json.load(open(path))["layouts"][key]
     except (OSError, KeyError, ValueError):
         return None
     cyc = lay["simd_cycles_per_64_nonces"]
@@ -204,7 +219,7 @@ def executed_roofline(nonces, kernel_ms, valu_pmc, pmc_src, valu_static, clock_g
     the kernel on this box.  The ceiling for this loop is its issue bound
     (issue_bound.frac); this fraction is below 1 by construction."""
     if valu_pmc:
-        v, src = valu_pmc, f"PMC SQ_INSTS_VALU x 64 / nonces ({pmc_src})"
+        v, src = valu_pmc, f"PMC SQ_INSTS_VALU x 64 / nonces (imported: {pmc_src})"
     elif valu_static:
         v, src = valu_static, "static count of the built inner loop (isa_mix.json)"
     else:
@@ -532,25 +547,43 @@ def pci_bus_id(device):
 
 def step_record(st):
     """What the line keeps of one call's bm_stats_t: nonces, GPU span, the
-    combine that ran and RCCL's view of the communicator, per device too."""
+    combine that ran and RCCL's view of the communicator, per device too, and
+    (ABI 7) what the combine and the start cost: the RCCL version, the
+    communicator's set-up time, the allgather's event pair (its wait for the
+    slowest peer included), the combine's host time, and each device's start
+    against the earliest device's."""
+    nd = st.devices
     return {"nonces": st.nonces, "span_ms": st.span_ms, "combine": COMBINED_NAMES.get(st.combine_used, "?"),
             "rccl_status": st.rccl_status, "rccl_nranks": st.rccl_nranks, "rccl_rank": st.rccl_rank,
-            "devices": [(st.dev_nonces[i], st.dev_span_ms[i]) for i in range(st.devices)],
-            "dev_rccl": [(st.dev_rccl_rank[i], st.dev_rccl_device[i]) for i in range(st.devices)]}
+            "devices": [(st.dev_nonces[i], st.dev_span_ms[i]) for i in range(nd)],
+            "dev_rccl": [(st.dev_rccl_rank[i], st.dev_rccl_device[i]) for i in range(nd)],
+            "rccl_version": getattr(st, "rccl_version", 0), "rccl_init_ms": getattr(st, "rccl_init_ms", 0.0),
+            "allgather_ms": getattr(st, "rccl_allgather_ms", 0.0), "combine_ms": getattr(st, "combine_ms", 0.0),
+            "start_threads": getattr(st, "start_threads", 1),
+            "dev_start_ms": [getattr(st, "dev_start_ms", [0.0] * nd)[i] for i in range(nd)],
+            "dev_allgather_ms": [getattr(st, "dev_allgather_ms", [0.0] * nd)[i] for i in range(nd)]}
 
 
-def rank_summary(rank, dev, pers, sysfs_clock):
+def rank_summary(rank, dev, pers, sysfs_clock, start_offset_ms=None):
     """One torchrun rank's share of the timed steps (pers: step() records):
     its GPU (HIP device and PCI bus id), nonces, GPU span and rate, the
     combine that ran, what RCCL reported about the communicator
     (ncclCommCount / ncclCommUserRank / ncclCommCuDevice; 0 / -1 without
-    one), and its GPU clock over the timed region."""
+    one), its GPU clock over the timed region, what its combine cost per step
+    (the allgather's HIP event pair, which includes the wait for the slowest
+    rank, and the combine's host time), and when it left the start barrier
+    against the earliest rank (wall clock, start_offset_ms)."""
     last = pers[-1]
     mine = {"rank": rank, "device": dev, "pci_bus_id": pci_bus_id(dev), "nonces": last["nonces"],
             "span_ms": round(_mean([p["span_ms"] for p in pers]), 3), "combine": last["combine"],
             "rccl_nranks": last["rccl_nranks"], "rccl_rank": last["rccl_rank"],
             "rccl_device": last["dev_rccl"][0][1] if last["dev_rccl"] else -1,
-            "clock_ghz_sysfs": None if sysfs_clock is None else round(sysfs_clock, 3)}
+            "clock_ghz_sysfs": None if sysfs_clock is None else round(sysfs_clock, 3),
+            "allgather_ms": round(_mean([p["allgather_ms"] for p in pers]), 4),
+            "combine_ms": round(_mean([p["combine_ms"] for p in pers]), 4),
+            "rccl_init_ms": round(last["rccl_init_ms"], 1)}
+    if start_offset_ms is not None:
+        mine["start_offset_ms"] = round(start_offset_ms, 3)
     mine["GHs"] = round(mine["nonces"] / mine["span_ms"] / 1e6, 3) if mine["span_ms"] > 0 else None
     if last["rccl_status"]:
         mine["rccl_status"] = last["rccl_status"]
@@ -569,8 +602,87 @@ def device_summaries(pers, device_ids):
         slots.append({"device": device_ids[i], "pci_bus_id": pci_bus_id(device_ids[i]), "nonces": nn,
                       "span_ms": round(sp, 3), "GHs": round(nn / sp / 1e6, 3) if sp > 0 else None,
                       "combine": last["combine"], "rccl_nranks": last["rccl_nranks"], "rccl_rank": r,
-                      "rccl_device": d})
+                      "rccl_device": d,
+                      # its first operation against the earliest device's (host
+                      # submission; bm_stats_t.dev_start_ms), and its allgather
+                      "start_ms": round(_mean([p["dev_start_ms"][i] for p in pers if i < len(p["dev_start_ms"])]),
+                                        4),
+                      "allgather_ms": round(_mean([p["dev_allgather_ms"][i] for p in pers
+                                                   if i < len(p["dev_allgather_ms"])]), 4),
+                      # the context's (one communicator set, one combine stage)
+                      "rccl_init_ms": round(last["rccl_init_ms"], 1),
+                      "combine_ms": round(_mean([p["combine_ms"] for p in pers]), 4)})
     return slots
+
+
+def rccl_version_str(v):
+    """ncclGetVersion's integer (e.g. 22703) as "2.27.3"."""
+    if not v:
+        return None
+    return f"{v // 10000}.{v // 100 % 100}.{v % 100}" if v >= 10000 else f"{v // 1000}.{v // 100 % 10}.{v % 100}"
+
+
+def rccl_costs(slots, version):
+    """N > 1: what the RCCL combine cost per step, from every slot's stats
+    (ABI 7): RCCL's version, the communicator's set-up time (the max over
+    slots: a rank's init includes its wait for the last rank to arrive), the
+    allgather's HIP event pair per step (min and max over slots: every pair
+    starts when its own slot's work is done, so it includes the wait for the
+    slowest slot, and the min is the closest to the bare collective), and the
+    combine stage's host time.  None, with the reason, when no slot combined
+    through RCCL (a rendezvous gather, host copies): there is nothing of RCCL
+    to report."""
+    if not slots or any(s["combine"] != "rccl" for s in slots):
+        return {"rccl": None, "rccl_absent": "combine " + "/".join(sorted({s["combine"] for s in slots}))
+                + ": no RCCL collective ran"}
+    ag = [s.get("allgather_ms", 0.0) for s in slots]
+    return {"rccl": {"version": version, "version_str": rccl_version_str(version),
+                     "init_ms": round(max(s.get("rccl_init_ms", 0.0) for s in slots), 1),
+                     "allgather_ms_min": round(min(ag), 4), "allgather_ms_max": round(max(ag), 4),
+                     "combine_ms_max": round(max(s.get("combine_ms", 0.0) for s in slots), 4),
+                     "per_step": "allgather_ms: HIP events around each slot's allgather on its stream, from the end "
+                                 "of its own work (so the wait for the slowest slot is inside); combine_ms: the "
+                                 "library's host time for the whole combine stage"}}
+
+
+def c4_block(args, ctx, grp, search, n):
+    """north_star's target is stated on a 2^40-nonce search, so
+    every line carries one C4 step ([0, 2^40-1], 'bradfitz', strong scaling:
+    the N GPUs split it) after the headline's timed region, through the same
+    context or group and the same split shares.  Warm: its layouts (P = 9..21,
+    1- to 13-digit nonces) live in the code objects the headline's steps
+    already loaded on every GPU.  Timed like the headline (barrier, one
+    search, barrier, max over ranks), checked against the committed golden
+    (the 2^40 CPU scan).  About 20 s on one GPU, 2.5 s on eight."""
+    msg, lo, hi, scaling, desc = workload("C4", n)
+    grp.barrier()
+    t_wall = time.time()
+    t = time.perf_counter()
+    res = search(msg, lo, hi)
+    dt = time.perf_counter() - t
+    rec = step_record(ctx.last_stats())
+    grp.barrier()
+    dt = grp.max(dt)
+    total = hi - lo + 1
+    want = golden(msg, lo, hi)
+    out = {"workload": desc, "lower": lo, "upper": hi, "nonces": total, "scaling": scaling,
+           "GHs": round(total / dt / 1e9, 4), "seconds": round(dt, 4), "result": list(res), "golden": want,
+           "result_ok": None if want is None else list(res) == want, "combine": rec["combine"]}
+    if grp.world > 1:
+        starts = grp.gather(t_wall)
+        slots = grp.gather({"rank": grp.rank, "nonces": rec["nonces"], "span_ms": round(rec["span_ms"], 3),
+                            "GHs": round(rec["nonces"] / rec["span_ms"] / 1e6, 3) if rec["span_ms"] > 0 else None,
+                            "combine": rec["combine"], "allgather_ms": round(rec["allgather_ms"], 4),
+                            "start_offset_ms": round((t_wall - min(starts)) * 1e3, 3)})
+        out["ranks"] = slots
+    else:
+        out["devices"] = [{"device": i, "nonces": nn, "span_ms": round(sp, 3),
+                           "GHs": round(nn / sp / 1e6, 3) if sp > 0 else None,
+                           "start_ms": round(rec["dev_start_ms"][i], 4) if i < len(rec["dev_start_ms"]) else None,
+                           "allgather_ms": round(rec["dev_allgather_ms"][i], 4)
+                           if i < len(rec["dev_allgather_ms"]) else None}
+                          for i, (nn, sp) in enumerate(rec["devices"])]
+    return out
 
 
 def scaling_validity(n, slots, want, rehearsal):
@@ -709,6 +821,9 @@ def main():
                          "whatever --steps the caller passes")
     ap.add_argument("--no-balance", action="store_true",
                     help="keep near-equal pieces (default: after the warmup, pieces follow each GPU's measured rate)")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the one warm C4 step ([0, 2^40-1], strong scaling; north_star's target) that every "
+                         "C2/C3 line carries after its timed region (about 20 s on one GPU, 2.5 s on eight)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N-way split on ONE GPU (all ranks / devices are GPU 0): exercises the multi-GPU "
                          "path on a one-GPU box; not a scaling measurement")
@@ -749,6 +864,7 @@ def main():
     sampler = ClockSampler(dev, period=0.05 if (args.clock_sample if args.clock_sample is not None else n > 1)
                            else None)
     grp.barrier()
+    t0_wall = time.time()  # when this rank left the barrier (wall clock: common to the node's ranks)
     sampler.start()
     t0 = time.perf_counter()
     doms = []
@@ -761,6 +877,9 @@ def main():
     grp.barrier()
     dt = grp.max(dt)
     clocks = grp.gather(sysfs_clock) if world > 1 else [sysfs_clock]
+    starts = grp.gather(t0_wall) if world > 1 else [t0_wall]
+    # north_star's 2^40 target, measured at every N: one warm C4 step
+    c4 = None if (args.no_c4 or args.config == "C4") else c4_block(args, ctx, grp, search, n)
     # the clock under the dominant kernel on THIS box, for the issue bound
     # (untimed, after the timed region; every rank on its own GPU)
     dom0 = doms[-1][0]
@@ -779,7 +898,7 @@ def main():
         # each rank's share of the timed steps: its nonces, its GPU span, its
         # rate, how the partials met (and what RCCL says about the
         # communicator), and its GPU clock (driver hwmon)
-        slots = grp.gather(rank_summary(grp.rank, dev, pers, sysfs_clock))
+        slots = grp.gather(rank_summary(grp.rank, dev, pers, sysfs_clock, (t0_wall - min(starts)) * 1e3))
         how += f"; combine {combine}"
     else:
         slots = device_summaries(pers, ([0] * n if args.rehearse_one_gpu else list(range(n))) if n > 1 else [dev])
@@ -807,6 +926,8 @@ def main():
         "result_ok": None if want is None else list(res) == want,
         "hip_runtime": hip_runtimes(),
     }
+    if c4 is not None:
+        out["c4"] = c4
     if n > 1:
         # what RCCL itself reported (ncclCommCount / UserRank / CuDevice per
         # rank or device) and whether the line measures N distinct GPUs
@@ -814,13 +935,24 @@ def main():
         out["rccl_nranks"] = (sorted({s["rccl_nranks"] for s in slots}) if world > 1
                               else pers[-1]["rccl_nranks"])
         out.update(scaling_validity(n, slots, args.combine if world > 1 else "rccl", args.rehearse_one_gpu))
+        # what RCCL cost per step (ABI 7), or why there is nothing of it
+        out.update(rccl_costs(slots, pers[-1]["rccl_version"]))
+        # the start of the timed steps: ranks leave the rendezvous barrier at
+        # slightly different moments (wall clock); the devices of one process
+        # each get their work from a host thread of their own (host submission
+        # times, bm_stats_t.dev_start_ms; max over devices, mean over steps)
+        if world > 1:
+            out["start_skew_ms"] = round((max(starts) - min(starts)) * 1e3, 3)
+        else:
+            out["start_skew_ms"] = round(_mean([max(p["dev_start_ms"] or [0.0]) for p in pers]), 4)
+            out["start_threads"] = pers[-1]["start_threads"]
     if dom is not None:
         ms = [d[0].ms for d in doms if d[0] is not None]
         dom_ms = sum(ms) / len(ms)
         c_eff = kernel_compressions(dom)  # blocks the kernel compresses per nonce
         c_survey = compressions_per_nonce(len(msg), dom.digits)
         achieved = dom.nonces * c_eff * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
-        kind = "c" if dom.pad_block == 2 else dom.nbv  # isa_mix.json key of the kernel
+        key = isa_key(dom.p, dom.nbv, dom.pad_block)  # isa_mix.json key of the kernel
         pmc, pmc_src = pmc_summary(args.config, dom.p, dom.nbv, dom.pad_block)
         pmc = pmc or {}
         cnt = pmc.get("counters", {})
@@ -831,13 +963,16 @@ def main():
                               "kernel compresses per nonce; not a ceiling -- the kernel executes fewer ops per "
                               "nonce than that count (see executed), so this can exceed 1 on layouts whose "
                               "constant words fold away (DESIGN.md §5)",
+                # the contract's field; PMC cannot run inside this timed process, so
+                # it is the committed pass's figure (roofline.pmc, imported)
                 "traffic": pmc.get("hbm_bytes_per_launch"),
                 "traffic_unit": "memory-side bytes per launch (PMC FETCH_SIZE+WRITE_SIZE)",
-                "traffic_note": "memory-side writes of the dequeue counter's returning atomics and of the rare "
-                                "path's spilled best (hash, nonce); the search reads no input from HBM "
-                                "(DESIGN.md §5, §8). FETCH_SIZE is not doubled: the guide's x2 is for 16-B/lane "
-                                "streaming reads, which this kernel does not issue",
-                "pmc_src": pmc_src,
+                "traffic_imported": bool(pmc),
+                "traffic_note": "imported from roofline.pmc.src (another run); memory-side writes of the dequeue "
+                                "counter's returning atomics and of the rare path's spilled best (hash, nonce); "
+                                "the search reads no input from HBM (DESIGN.md §5, §8). FETCH_SIZE is not "
+                                "doubled: the guide's x2 is for 16-B/lane streaming reads, which this kernel "
+                                "does not issue",
                 "kernel": f"{kernel_name(dom.p, dom.nbv, dom.pad_block)} ({dom.digits}-digit nonces)",
                 "kernel_ms": round(dom_ms, 3), "kernel_nonces": dom.nonces,
                 "compressions_per_nonce": c_eff, "ops_per_nonce": c_eff * OPS_PER_COMPRESSION,
@@ -848,20 +983,29 @@ def main():
             roof["survey_compressions_per_nonce"] = c_survey
             roof["survey_frac"] = round(dom.nonces * c_survey * OPS_PER_COMPRESSION / (dom_ms * 1e-3) / 1e12
                                         / VALU_PEAK_T, 4)
-        if pmc.get("valu_per_nonce"):  # SQ_INSTS_VALU x 64 lanes / the profiled launch's nonces
-            roof["valu_per_nonce_pmc"] = round(pmc["valu_per_nonce"], 1)
-        elif "SQ_INSTS_VALU" in cnt and n == 1 and world == 1:
-            # an older summary without the profiled launch's nonces: the PMC pass
-            # ran this config's N = 1 call, whose dominant launch is this one
-            roof["valu_per_nonce_pmc"] = round(cnt["SQ_INSTS_VALU"] * 64 / dom.nonces, 1)
-        if "SQ_ACTIVE_INST_VALU2" in cnt and cnt.get("SQ_INSTS_VALU"):
-            roof["valu_dual_issued_frac_pmc"] = round(cnt["SQ_ACTIVE_INST_VALU2"] / cnt["SQ_INSTS_VALU"], 4)
-        if clock:
-            roof["clock_ghz_pmc"] = round(clock, 3)
+        # every PMC-derived figure sits under roofline.pmc, marked
+        # as imported from the committed rocprofv3 pass (another run, maybe
+        # another box, at that box's clock) -- never measured by this run
+        pm = {"src": pmc_src, "imported": True,
+              "note": "rocprofv3 --pmc passes cannot run inside this timed process: these figures are the "
+                      "committed summary's (tools/pmc_summary.py), not this run's"} if pmc else None
+        if pm is not None:
+            if pmc.get("valu_per_nonce"):  # SQ_INSTS_VALU x 64 lanes / the profiled launch's nonces
+                pm["valu_per_nonce"] = round(pmc["valu_per_nonce"], 1)
+            elif "SQ_INSTS_VALU" in cnt and n == 1 and world == 1:
+                # an older summary without the profiled launch's nonces: the PMC pass
+                # ran this config's N = 1 call, whose dominant launch is this one
+                pm["valu_per_nonce"] = round(cnt["SQ_INSTS_VALU"] * 64 / dom.nonces, 1)
+            if "SQ_ACTIVE_INST_VALU2" in cnt and cnt.get("SQ_INSTS_VALU"):
+                pm["valu_dual_issued_frac"] = round(cnt["SQ_ACTIVE_INST_VALU2"] / cnt["SQ_INSTS_VALU"], 4)
+            if clock:
+                pm["box_clock_ghz"] = round(clock, 3)
+            pm["hbm_bytes_per_launch"] = pmc.get("hbm_bytes_per_launch")
+        roof["pmc"] = pm
         # the clock under the dominant kernel on this box: live stamps
         # (s_memtime / s_memrealtime, BM_CLOCK_PROBE builds), else the
         # driver's gfx clock sampled while that kernel's range ran alone
-        # (measure_clock).  The committed PMC clock (clock_ghz_pmc) is another
+        # (measure_clock).  The committed PMC clock (roofline.pmc) is another
         # run, maybe another box: it is never used for the fraction.
         live = [d[0].clock_ghz for d in doms if d[0] is not None and d[0].clock_ghz > 0]
         live_clock = sum(live) / len(live) if live else None
@@ -882,7 +1026,7 @@ def main():
             if box.get("cap_w"):
                 roof["power_cap_w"] = round(box["cap_w"], 1)
         ib_clock = live_clock or box.get("ghz_live") or box.get("ghz")
-        ib = issue_bound(dom.p, kind, ib_clock or clock or 0.0) if (ib_clock or clock) else None
+        ib = issue_bound(key, ib_clock or clock or 0.0) if (ib_clock or clock) else None
         if ib:
             if ib_clock:
                 where = (f"{box.get('searches')} untimed searches of the dominant kernel's range "
@@ -892,12 +1036,12 @@ def main():
                                    if box.get("ghz_live") else f"hwmon freq1_input every 10 ms over {where}")
                 ib["frac"] = round(dom.nonces / (dom_ms * 1e-3) / 1e9 / ib["GHs_per_gpu"], 4)
             else:
-                ib["clock_src"] = pmc_src
+                ib["clock_src"] = f"imported: {pmc_src}"
                 ib["note"] = "no clock measured on this box: the bound at the committed PMC clock, no frac"
             ib["role"] = "ceiling: the loop's own issue bound at the measured clock (DESIGN.md §5)"
             roof["issue_bound"] = ib
-        static = issue_bound(dom.p, kind, 1.0)  # the built loop's static VALU count
-        roof["executed"] = executed_roofline(dom.nonces, dom_ms, roof.get("valu_per_nonce_pmc"), pmc_src,
+        static = issue_bound(key, 1.0)  # the built loop's static VALU count
+        roof["executed"] = executed_roofline(dom.nonces, dom_ms, (pm or {}).get("valu_per_nonce"), pmc_src,
                                              static and static["valu_per_nonce"], ib_clock)
         if calls:
             roof["call"] = call_roofline(calls, ctx.last_stats().launches, pers[-1]["nonces"],

@@ -24,7 +24,8 @@ BM_ETIMEDOUT = -8
 BM_MAX_LAUNCH_STATS = 64
 BM_MAX_STAT_DEVICES = 16
 BM_RCCL_ID_BYTES = 128
-BM_ABI_VERSION = 6
+BM_ABI_VERSION = 7
+BM_DEFAULT_PEER_TIMEOUT_MS = 600_000
 BM_COMBINE_AUTO, BM_COMBINE_RCCL, BM_COMBINE_HOST = 0, 1, 2
 # bm_stats_t.combine_used
 BM_COMBINED_NONE, BM_COMBINED_RCCL, BM_COMBINED_HOST, BM_COMBINED_LOCAL = 0, 1, 2, 3
@@ -52,7 +53,14 @@ class Stats(ctypes.Structure):
                 ("combine_used", c_i32), ("rccl_status", c_i32), ("devices", c_u32), ("reserved", c_u32),
                 ("dev_nonces", c_u64 * BM_MAX_STAT_DEVICES), ("dev_span_ms", ctypes.c_double * BM_MAX_STAT_DEVICES),
                 ("rccl_nranks", c_i32), ("rccl_rank", c_i32), ("dev_rccl_rank", c_i32 * BM_MAX_STAT_DEVICES),
-                ("dev_rccl_device", c_i32 * BM_MAX_STAT_DEVICES), ("launch", LaunchStat * BM_MAX_LAUNCH_STATS)]
+                ("dev_rccl_device", c_i32 * BM_MAX_STAT_DEVICES),
+                # ABI 7: the RCCL version, the communicator's set-up time, the allgather's
+                # event pair and each device's start against the earliest device's
+                ("rccl_version", c_i32), ("start_threads", c_i32), ("rccl_init_ms", ctypes.c_double),
+                ("rccl_allgather_ms", ctypes.c_double), ("combine_ms", ctypes.c_double),
+                ("dev_allgather_ms", ctypes.c_double * BM_MAX_STAT_DEVICES),
+                ("dev_start_ms", ctypes.c_double * BM_MAX_STAT_DEVICES),
+                ("launch", LaunchStat * BM_MAX_LAUNCH_STATS)]
 
 
 class Segment(ctypes.Structure):
@@ -119,6 +127,7 @@ def _open(path):
         "bm_ctx_rank_joined": ([vp, P(ctypes.c_int)], ctypes.c_int),
         "bm_ctx_set_peer_timeout": ([vp, ctypes.c_int], ctypes.c_int),
         "bm_ctx_set_test_rccl_fault": ([vp, ctypes.c_int], ctypes.c_int),
+        "bm_ctx_set_test_start_delay": ([vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "bm_ctx_rank": ([vp, P(ctypes.c_int), P(ctypes.c_int)], ctypes.c_int),
         "bm_reduce_gpu": ([vp, P(Result), ctypes.c_size_t, P(Result)], ctypes.c_int),
         "bm_ctx_set_test_fault": ([vp, ctypes.c_int], ctypes.c_int),
@@ -292,6 +301,11 @@ class Context:
 
     def set_test_rccl_fault(self, where: int):
         check(self._lib.bm_ctx_set_test_rccl_fault(self.handle, where), "bm_ctx_set_test_rccl_fault")
+
+    def set_test_start_delay(self, device: int, delay_us: int):
+        """Test hook: hold back device `device`'s submission by delay_us at
+        the start of every later search (a late-starting GPU)."""
+        check(self._lib.bm_ctx_set_test_start_delay(self.handle, device, delay_us), "bm_ctx_set_test_start_delay")
 
     def reduce(self, pairs):
         """Lexicographic min of (hash, nonce) pairs by the GPU reductions

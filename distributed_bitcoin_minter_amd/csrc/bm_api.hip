@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <chrono>
 #include <cstdarg>
@@ -20,6 +21,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -29,10 +31,12 @@
 
 namespace bm {
 
-// search kernel table [nbv-1][P], filled by bm_inst.hip at load time; row 2
-// holds search_kernel_padc<P> (P >= 55: a one-block message's padding-block
-// layouts with their constants folded)
-static const void* g_search[3][64];
+// search kernel table [nbv-1][P], filled by bm_inst.hip at load time; rows
+// 2 + K hold the padding-block layouts (P >= 55) with their constants folded
+// after K whole prefix blocks: search_kernel_padc<P> (K = 0, a one-block
+// message) and search_kernel_padk<P, K> (K = 1, 2)
+constexpr int kSearchRows = 3 + kMaxPadPrefixBlocks;
+static const void* g_search[kSearchRows][64];
 
 constexpr int kMaxInnerDigits = 2;  // S <= 100 nonces per task: small dequeue chunks, short tail
 constexpr uint32_t kNoncesPerLaneChunk = 100;  // default nonces per lane per dequeue (BTCMINER_CHUNK)
@@ -84,8 +88,11 @@ struct DeviceCtx {
     hipStream_t aux[kMaxStreams - 1] = {};  // extra launch streams (ctx->streams > 1)
     hipEvent_t fork = nullptr, join[kMaxStreams - 1] = {};
     hipEvent_t bal[2] = {};     // the device's first op and the end of its reduction (balance, timing)
+    hipEvent_t ag[2] = {};      // around the device's allgather (timing): its wait for the peers + transfer
     hipEvent_t own_done = nullptr;  // rank contexts: this rank's reduction done (before the allgather)
     uint64_t piece_nonces = 0;  // nonces of the device's piece in the last call
+    std::chrono::steady_clock::time_point submitted{};  // host time of the call's first op on this device
+    int test_delay_us = 0;      // test hook: hold back this device's submission (bm_ctx_set_test_start_delay)
     ncclComm_t comm = nullptr;  // multi-device ctx: ncclCommInitAll; joined rank ctx: the process group's
     std::vector<std::pair<const void*, int>> occ;  // kernel -> blocks per CU
     double wall_clock_hz = 100e6;                  // s_memrealtime rate
@@ -108,6 +115,7 @@ struct JoinJob {
     bool done = false, abandoned = false;
     ncclComm_t comm = nullptr;
     int rc = BM_ERCCL;
+    double init_ms = 0.0;  // the init's host time, until it settled
 };
 
 namespace {
@@ -161,14 +169,16 @@ struct bm_ctx {
     bool rank_ctx = false;    // made by bm_ctx_create_rank_local (one device, one slot of `world`)
     bool joined = false;      // rank ctx: member of an RCCL group (devs[0].comm)
     int group_status = 0;     // joined rank ctx whose communicator failed (BM_ERCCL / BM_ETIMEDOUT)
-    int peer_timeout_ms = 0;  // joined rank ctx: wait at most this long for the group (0: no limit)
+    int peer_timeout_ms = BM_DEFAULT_PEER_TIMEOUT_MS;  // joined rank ctx: wait at most this long for
+                                                       // the group (0: no limit)
+    double rccl_init_ms = 0.0;  // host time the current communicator(s) took to form
     int fault_after = -1;     // test hook: fail after enqueueing this many launches (-1: off)
     int test_rccl_fault = 0;  // test hook: 1 communicator set-up fails, 2 every allgather fails,
                               // 3 the gathered slots report a failed peer (rank groups)
     uint64_t lane_chunk = bm::kNoncesPerLaneChunk;  // nonces per lane per dequeue, at most (BTCMINER_CHUNK)
     std::vector<uint32_t> shares;  // the partitioner's shares per slot (empty: near-equal pieces)
     bool balance = false;          // multi-device: shares follow each device's measured rate
-    bool padc = true;              // use search_kernel_padc where it applies (BTCMINER_PADC=0: never; A/B knob)
+    bool padc = true;              // use search_kernel_padc / _padk where they apply (BTCMINER_PADC=0: never; A/B knob)
     // rank ctx: a join whose caller timed out while its worker was still
     // inside RCCL (the worker aborts the communicator if it ever gets one)
     std::shared_ptr<bm::JoinJob> pending_join;
@@ -177,7 +187,7 @@ struct bm_ctx {
 };
 
 extern "C" void bm_register_search_kernel(int p, int nbv, const void* fn) {
-    if (p >= 0 && p < 64 && nbv >= 1 && nbv <= 3) bm::g_search[nbv - 1][p] = fn;
+    if (p >= 0 && p < 64 && nbv >= 1 && nbv <= bm::kSearchRows) bm::g_search[nbv - 1][p] = fn;
 }
 
 namespace bm {
@@ -196,25 +206,37 @@ int blocks_per_cu(bm_ctx* ctx, DeviceCtx& d, const void* fn) {
 // Size one launch: S = 10^ms nonces per task (ms <= digits of word LW),
 // chunks of 64*m tasks dequeued per wave, and at most one resident grid of
 // workgroups (any surplus workgroup simply finds the counter exhausted).
-// The PADC kernel applies when the segment's state before the varying block
-// is the IV and its padding block is the one of a one-block message ending
-// at byte P (bm_kernels.hpp pad_kw_const): the constants it folds.
-bool padc_applies(const bm_segment_t& s) {
-    if (!s.pad_block || s.nbv != 1 || s.p < 55) return false;
-    for (int q = 0; q < 8; ++q)
-        if (s.mid[q] != kIV256[q]) return false;
-    const KW64 kw = pad_kw_const(s.p);
+// A folded padding-block kernel applies when the segment's padding block is
+// the one of a message of K whole blocks plus the varying block ending at
+// byte P (bm_sha256.hpp pad_kw_const(P, K), K <= kMaxPadPrefixBlocks), and for
+// K = 0 its entering state is the IV: the constants the kernel folds.
+// Returns K, or -1 when the generic kernel must run.
+int pad_fold_k(const bm_segment_t& s) {
+    if (!s.pad_block || s.nbv != 1 || s.p < 55) return -1;
     uint32_t w[64];
     for (int i = 0; i < 16; ++i) w[i] = s.pad_w[i];
     host::expand(w);
-    for (int t = 0; t < 64; ++t)
-        if (kK256[t] + w[t] != kw.v[t]) return false;
-    return true;
+    for (int k = 0; k <= kMaxPadPrefixBlocks; ++k) {
+        const KW64 kw = pad_kw_const(s.p, k);
+        bool same = true;
+        for (int t = 0; t < 64 && same; ++t) same = kK256[t] + w[t] == kw.v[t];
+        if (!same) continue;
+        if (k == 0)
+            for (int q = 0; q < 8; ++q)
+                if (s.mid[q] != kIV256[q]) return -1;
+        return k;
+    }
+    return -1;
 }
 
 int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_off, Launch& L) {
-    const bool padc = ctx->padc && padc_applies(s);
-    const void* fn = padc ? g_search[2][s.p] : g_search[s.nbv - 1][s.p];
+    // the folded kernel where it applies and this build registered it (an
+    // A/B build may instantiate only some layouts): else the generic one,
+    // which gives the same answer
+    const int fk = ctx->padc ? pad_fold_k(s) : -1;
+    const void* fn = fk >= 0 ? g_search[2 + fk][s.p] : nullptr;
+    const bool padc = fn != nullptr;
+    if (!fn) fn = g_search[s.nbv - 1][s.p];
     if (!fn) return BM_EINTERNAL;
     int ms = std::max(1, std::min(s.max_inner, kMaxInnerDigits));
     // word LW holds one digit: the kernel steps the next one in word LW-1
@@ -269,7 +291,7 @@ int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_
     std::memset(&L.stat, 0, sizeof L.stat);
     L.stat.p = s.p;
     L.stat.nbv = s.nbv;
-    L.stat.pad_block = padc ? 2 : s.pad_block;
+    L.stat.pad_block = padc ? 2 + fk : s.pad_block;
     L.stat.digits = s.digits;
     L.stat.inner_digits = ms;
     L.stat.nonces = s.vhi - s.vlo + 1;
@@ -325,6 +347,7 @@ int init_device(DeviceCtx& d, int id, int nslots) {
     BM_HIP(hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
     for (auto& e : d.join) BM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : d.bal) BM_HIP(hipEventCreate(&e));
+    for (auto& e : d.ag) BM_HIP(hipEventCreate(&e));
     BM_HIP(hipEventCreateWithFlags(&d.own_done, hipEventDisableTiming));
     int rc = ensure_counters(d, 256);
     if (rc != BM_OK) return rc;
@@ -357,6 +380,8 @@ void destroy_device(DeviceCtx& d) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : d.bal)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : d.ag)
+        if (e) (void)hipEventDestroy(e);
     if (d.fork) (void)hipEventDestroy(d.fork);
     for (auto& s : d.aux)
         if (s) (void)hipStreamDestroy(s);
@@ -380,7 +405,9 @@ int ensure_nccl(bm_ctx* ctx) {
     std::vector<ncclComm_t> comms(n);
     std::vector<int> ids(n);
     for (int i = 0; i < n; ++i) ids[i] = ctx->devs[i].id;
+    const auto t0 = std::chrono::steady_clock::now();
     if (ncclCommInitAll(comms.data(), n, ids.data()) != ncclSuccess) return BM_ERCCL;
+    ctx->rccl_init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (int i = 0; i < n; ++i) ctx->devs[i].comm = comms[i];
     ctx->nccl_ready = true;
     return BM_OK;
@@ -396,6 +423,7 @@ void abort_nccl(bm_ctx* ctx) {
         d.comm = nullptr;
     }
     ctx->nccl_ready = false;
+    ctx->rccl_init_ms = 0.0;
 }
 
 // A non-blocking communicator's last operation: wait until it leaves
@@ -412,6 +440,7 @@ int comm_settle(ncclComm_t comm, ncclResult_t r, std::chrono::steady_clock::time
 void join_worker(std::shared_ptr<JoinJob> job, int dev, int world, int rank, ncclUniqueId u) {
     ncclComm_t comm = nullptr;
     int rc = BM_ERCCL;
+    const auto t0 = std::chrono::steady_clock::now();
     if (hipSetDevice(dev) == hipSuccess) {
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.blocking = 0;
@@ -436,6 +465,8 @@ void join_worker(std::shared_ptr<JoinJob> job, int dev, int world, int rank, ncc
             if (!comm || (rc == BM_OK && !job->abandoned)) {
                 job->comm = comm;
                 job->rc = rc;
+                job->init_ms =
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 job->done = true;
                 job->cv.notify_all();
                 return;
@@ -461,59 +492,86 @@ void drain(bm_ctx* ctx) {
     (void)hipGetLastError();
 }
 
-// Stage 2 of a search: enqueue every launch and the second-pass reduction
-// of each device (its partial lands in d_slot).  On failure the caller drains.
+// Stage 2 of a search, one device: enqueue its launches and its second-pass
+// reduction (its partial lands in d_slot).  `enqueued` counts launches over
+// every device (the test fault).  On failure the caller drains.
+int enqueue_device(bm_ctx* ctx, int di, std::vector<Launch>& launches, uint32_t& first,
+                   std::atomic<int>& enqueued) {
+    DeviceCtx& d = ctx->devs[di];
+    const bool mark = ctx->balance || ctx->timing;  // per-device span events
+    BM_HIP(hipSetDevice(d.id));
+    if (d.test_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(d.test_delay_us));
+    // the call's first op on this device: its stream is idle, so it starts
+    // about when it is submitted (the common start of bm_stats_t.dev_start_ms)
+    if (mark) BM_HIP(hipEventRecord(d.bal[0], d.stream));
+    d.submitted = std::chrono::steady_clock::now();
+    uint32_t nparts = 0, li = 0;
+    if (!launches.empty())
+        BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches.size() * kCtrStride * sizeof(unsigned long long), d.stream));
+    // stream of each launch: biggest first, round-robin over the streams
+    const int ns = std::max(1, std::min<int>(ctx->streams, (int)launches.size()));
+    std::vector<uint32_t> order(launches.size());
+    for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
+    if (ns > 1) {
+        std::stable_sort(order.begin(), order.end(),
+                         [&](uint32_t x, uint32_t y) { return launches[x].stat.nonces > launches[y].stat.nonces; });
+        BM_HIP(hipEventRecord(d.fork, d.stream));
+        for (int k = 0; k + 1 < ns; ++k) BM_HIP(hipStreamWaitEvent(d.aux[k], d.fork, 0));
+    }
+    if (!order.empty()) first = order[0];
+    for (uint32_t r = 0; r < order.size(); ++r) {
+        li = order[r];
+        Launch& L = launches[li];
+        hipStream_t s = (r % ns) == 0 ? d.stream : d.aux[r % ns - 1];
+        if (ctx->fault_after >= 0 && enqueued.fetch_add(1) >= ctx->fault_after) return BM_EINTERNAL;  // test hook
+        const bool timed = ctx->timing && li < (uint32_t)kEventPairs;
+        if (timed) BM_HIP(hipEventRecord(d.ev[2 * li], s));
+        unsigned long long* ctr = d.d_ctr + kCtrStride * li;
+        void* kargs[] = {&L.args, &d.d_part, &ctr};
+        BM_HIP(hipLaunchKernel(L.fn, dim3(L.grid), dim3(kBlock), kargs, 0, s));
+        if (timed) BM_HIP(hipEventRecord(d.ev[2 * li + 1], s));
+        nparts += L.grid;
+    }
+    for (int k = 0; k + 1 < ns; ++k) {
+        BM_HIP(hipEventRecord(d.join[k], d.aux[k]));
+        BM_HIP(hipStreamWaitEvent(d.stream, d.join[k], 0));
+    }
+    // nparts = 0 (a device or rank with nothing to scan) writes (2^64-1, 2^64-1)
+    reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, &d.d_slot->p);
+    BM_HIP(hipGetLastError());
+    if (mark) BM_HIP(hipEventRecord(d.bal[1], d.stream));
+    if (BM_CLOCK_PROBE && ctx->timing && !launches.empty())  // clock stamps, for the launch stats
+        BM_HIP(hipMemcpyAsync(d.h_ctr, d.d_ctr, launches.size() * kCtrStride * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost, d.stream));
+    return BM_OK;
+}
+
+// Stage 2 of a search: every device's work.  A context of several devices
+// submits each device's work from a host thread of its own, so device N-1
+// does not wait for the other devices' ~15 API calls each before it starts
+// (the start skew of a serial submission; bm_stats_t.dev_start_ms reports
+// what is left of it).
 int enqueue(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches, std::vector<uint32_t>& first) {
     const int ndev = (int)ctx->devs.size();
-    const bool mark = ctx->balance || ctx->timing;  // per-device span events
     if (ctx->fault_after == 0) return BM_EINTERNAL;  // test hook (also for a rank with nothing to scan)
-    int enqueued = 0;
-    for (int di = 0; di < ndev; ++di) {
-        DeviceCtx& d = ctx->devs[di];
-        BM_HIP(hipSetDevice(d.id));
-        uint32_t nparts = 0, li = 0;
-        if (!launches[di].empty())
-            BM_HIP(hipMemsetAsync(d.d_ctr, 0, launches[di].size() * kCtrStride * sizeof(unsigned long long),
-                                  d.stream));
-        if (mark) BM_HIP(hipEventRecord(d.bal[0], d.stream));
-        // stream of each launch: biggest first, round-robin over the streams
-        const int ns = std::max(1, std::min<int>(ctx->streams, (int)launches[di].size()));
-        std::vector<uint32_t> order(launches[di].size());
-        for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
-        if (ns > 1) {
-            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-                return launches[di][a].stat.nonces > launches[di][b].stat.nonces;
-            });
-            BM_HIP(hipEventRecord(d.fork, d.stream));
-            for (int k = 0; k + 1 < ns; ++k) BM_HIP(hipStreamWaitEvent(d.aux[k], d.fork, 0));
+    std::atomic<int> enqueued{0};
+    ctx->stats.start_threads = 1;
+    if (ndev == 1) return enqueue_device(ctx, 0, launches[0], first[0], enqueued);
+    std::vector<int> rc(ndev, BM_OK);
+    std::vector<std::thread> th;
+    th.reserve(ndev - 1);
+    for (int di = 1; di < ndev; ++di) {
+        try {
+            th.emplace_back([&, di] { rc[di] = enqueue_device(ctx, di, launches[di], first[di], enqueued); });
+        } catch (const std::system_error&) {  // no thread: this one submits that device's work itself
+            rc[di] = enqueue_device(ctx, di, launches[di], first[di], enqueued);
         }
-        if (!order.empty()) first[di] = order[0];
-        for (uint32_t r = 0; r < order.size(); ++r) {
-            li = order[r];
-            Launch& L = launches[di][li];
-            hipStream_t s = (r % ns) == 0 ? d.stream : d.aux[r % ns - 1];
-            if (ctx->fault_after >= 0 && enqueued == ctx->fault_after) return BM_EINTERNAL;  // test hook
-            const bool timed = ctx->timing && li < (uint32_t)kEventPairs;
-            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li], s));
-            unsigned long long* ctr = d.d_ctr + kCtrStride * li;
-            void* kargs[] = {&L.args, &d.d_part, &ctr};
-            BM_HIP(hipLaunchKernel(L.fn, dim3(L.grid), dim3(kBlock), kargs, 0, s));
-            ++enqueued;
-            if (timed) BM_HIP(hipEventRecord(d.ev[2 * li + 1], s));
-            nparts += L.grid;
-        }
-        for (int k = 0; k + 1 < ns; ++k) {
-            BM_HIP(hipEventRecord(d.join[k], d.aux[k]));
-            BM_HIP(hipStreamWaitEvent(d.stream, d.join[k], 0));
-        }
-        // nparts = 0 (a device or rank with nothing to scan) writes (2^64-1, 2^64-1)
-        reduce_partials<<<1, kReduceThreads, 0, d.stream>>>(d.d_part, nparts, &d.d_slot->p);
-        BM_HIP(hipGetLastError());
-        if (mark) BM_HIP(hipEventRecord(d.bal[1], d.stream));
-        if (BM_CLOCK_PROBE && ctx->timing && !launches[di].empty())  // clock stamps, for the launch stats
-            BM_HIP(hipMemcpyAsync(d.h_ctr, d.d_ctr, launches[di].size() * kCtrStride * sizeof(unsigned long long),
-                                  hipMemcpyDeviceToHost, d.stream));
     }
+    rc[0] = enqueue_device(ctx, 0, launches[0], first[0], enqueued);
+    for (auto& t : th) t.join();
+    ctx->stats.start_threads = 1 + (int)th.size();
+    for (int r : rc)
+        if (r != BM_OK) return r;
     return BM_OK;
 }
 
@@ -540,6 +598,19 @@ void record_rccl(bm_ctx* ctx, bool used) {
             st.dev_rccl_rank[di] = r;
             st.dev_rccl_device[di] = dev;
         }
+    }
+}
+
+// The allgather's event pair on each device (timing on; the streams have
+// been synchronised): bm_stats_t.dev_allgather_ms and their max.
+void record_allgather(bm_ctx* ctx) {
+    bm_stats_t& st = ctx->stats;
+    for (size_t di = 0; di < ctx->devs.size() && di < (size_t)BM_MAX_STAT_DEVICES; ++di) {
+        DeviceCtx& d = ctx->devs[di];
+        float ms = 0.f;
+        if (hipSetDevice(d.id) != hipSuccess || hipEventElapsedTime(&ms, d.ag[0], d.ag[1]) != hipSuccess) continue;
+        st.dev_allgather_ms[di] = ms;
+        st.rccl_allgather_ms = std::max(st.rccl_allgather_ms, (double)ms);
     }
 }
 
@@ -572,7 +643,8 @@ int combine_local(bm_ctx* ctx, Partial* best_out) {
                 for (int di = 0; di < ndev && rc == BM_OK; ++di) {
                     DeviceCtx& d = ctx->devs[di];
                     if (hipSetDevice(d.id) != hipSuccess ||
-                        hipMemsetAsync(&d.d_slot->status, 0, 2 * sizeof(uint64_t), d.stream) != hipSuccess)
+                        hipMemsetAsync(&d.d_slot->status, 0, 2 * sizeof(uint64_t), d.stream) != hipSuccess ||
+                        (ctx->timing && hipEventRecord(d.ag[0], d.stream) != hipSuccess))
                         return BM_EHIP;
                 }
                 if (ctx->test_rccl_fault == 2) {
@@ -587,6 +659,14 @@ int combine_local(bm_ctx* ctx, Partial* best_out) {
                             rc = BM_ERCCL;
                     }
                     if (ncclGroupEnd() != ncclSuccess) rc = BM_ERCCL;
+                }
+                // the allgather's span on each device: from the end of its own
+                // reduction (recorded before the collective was enqueued) to the
+                // collective's end, so it includes the wait for the slowest device
+                for (int di = 0; di < ndev && rc == BM_OK && ctx->timing; ++di) {
+                    DeviceCtx& d = ctx->devs[di];
+                    if (hipSetDevice(d.id) != hipSuccess || hipEventRecord(d.ag[1], d.stream) != hipSuccess)
+                        return BM_EHIP;
                 }
             }
             if (rc == BM_OK) {
@@ -620,6 +700,7 @@ int combine_local(bm_ctx* ctx, Partial* best_out) {
     st.combine_used = ctx->rank_ctx ? BM_COMBINED_LOCAL : via_rccl ? BM_COMBINED_RCCL : BM_COMBINED_HOST;
     st.rccl_status = ctx->rccl_status;
     record_rccl(ctx, via_rccl);
+    if (via_rccl && ctx->timing) record_allgather(ctx);
     *best_out = lex_min_slots(ctx->devs[0].h_slots, nslots);
     return BM_OK;
 }
@@ -661,8 +742,12 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
         // non-blocking communicator may first report ncclInProgress: then it
         // is enqueued once the communicator settles)
         const auto timeout = std::chrono::milliseconds(ctx->peer_timeout_ms);
+        const bool ag_timed = ctx->timing && hipEventRecord(d.ag[0], d.stream) == hipSuccess;
         rc = comm_settle(d.comm, ncclAllGather(d.d_slot, d.d_gather, kSlotWords, ncclUint64, d.comm, d.stream),
                          std::chrono::steady_clock::now() + timeout, limited);
+        // the allgather's span on this rank's stream: from the end of its own
+        // work to the end of the collective (the wait for the slowest rank included)
+        if (rc == BM_OK && ag_timed) (void)hipEventRecord(d.ag[1], d.stream);
         // a failed copy of the gathered slots is this rank's own error: the
         // collective itself still runs, so the communicator stays good
         copied = rc == BM_OK && hipMemcpyAsync(d.h_slots, d.d_gather, sizeof(Slot) * world,
@@ -700,6 +785,7 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
     }
     st.combine_used = BM_COMBINED_RCCL;
     record_rccl(ctx, true);
+    if (ctx->timing) record_allgather(ctx);
     if (!copied) return own_rc != BM_OK ? own_rc : BM_EHIP;
     // test hook: the last slot arrives carrying a peer's failure status, as
     // a real peer's would (at world 1 that slot is this rank's own)
@@ -770,6 +856,25 @@ int plan_launches(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, u
     return BM_OK;
 }
 
+// The RCCL figures every call reports, whatever its outcome: the library's
+// RCCL version and, while the context holds a communicator, the time it took
+// to form.
+int rccl_version() {
+    static const int v = [] {
+        int x = 0;
+        return ncclGetVersion(&x) == ncclSuccess ? x : 0;
+    }();
+    return v;
+}
+
+void stamp_common(bm_ctx* ctx) {
+    bm_stats_t& st = ctx->stats;
+    st.rccl_version = rccl_version();
+    const bool have = ctx->rank_ctx ? ctx->joined && ctx->devs[0].comm != nullptr : ctx->nccl_ready;
+    st.rccl_init_ms = have ? ctx->rccl_init_ms : 0.0;
+    if (st.start_threads == 0) st.start_threads = 1;
+}
+
 int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, bm_result_t* out) {
     const auto t_start = std::chrono::steady_clock::now();
     bm_stats_t& st = ctx->stats;
@@ -779,9 +884,11 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
     const bool group = ctx->rank_ctx && ctx->joined;
     if (group && ctx->group_status != BM_OK) {  // the communicator failed earlier: leave the group first
         st.rccl_status = ctx->group_status;
+        stamp_common(ctx);
         return ctx->group_status;
     }
     if (lower > upper) {  // miner.go:45-46 with zero iterations (every rank sees the same range)
+        stamp_common(ctx);
         out->hash = UINT64_MAX;
         out->nonce = UINT64_MAX;
         return BM_OK;
@@ -798,6 +905,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
 
     // 3. combine (a rank of a group takes part even after a failure)
     Partial best{UINT64_MAX, UINT64_MAX};
+    const auto t_combine = std::chrono::steady_clock::now();
     if (group) {
         const int grc = combine_group(ctx, rc, &best);
         if (grc != BM_OK) {
@@ -806,6 +914,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
             std::memset(&st, 0, sizeof st);
             record_rccl(ctx, false);
             st.rccl_status = keep;
+            stamp_common(ctx);
             return grc;
         }
     } else {
@@ -814,11 +923,24 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
             drain(ctx);
             std::memset(&st, 0, sizeof st);
             record_rccl(ctx, false);
+            stamp_common(ctx);
             return rc;
         }
     }
+    st.combine_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_combine).count();
 
-    // 4. balance: the next call's shares follow each device's measured rate
+    // each device's start against the earliest device's (host submission times)
+    std::vector<double> start_ms(ndev, 0.0);
+    {
+        auto t0 = ctx->devs[0].submitted;
+        for (const auto& d : ctx->devs) t0 = std::min(t0, d.submitted);
+        for (int di = 0; di < ndev; ++di)
+            start_ms[di] = std::chrono::duration<double, std::milli>(ctx->devs[di].submitted - t0).count();
+    }
+
+    // 4. balance: the next call's shares follow each device's measured rate,
+    // its nonces over the time from the call's common start to its reduction,
+    // so a device that starts late gets a smaller piece
     if (ctx->balance && ndev > 1) {
         std::vector<double> rate(ndev, 0.0);
         bool ok = true;
@@ -827,7 +949,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
             float ms = 0.f;
             ok = d.piece_nonces >= kBalanceMinNonces && hipSetDevice(d.id) == hipSuccess &&
                  hipEventElapsedTime(&ms, d.bal[0], d.bal[1]) == hipSuccess && ms > 0.f;
-            if (ok) rate[di] = (double)d.piece_nonces / ms;
+            if (ok) rate[di] = (double)d.piece_nonces / (start_ms[di] + ms);
         }
         if (ok) {
             const double top = *std::max_element(rate.begin(), rate.end());
@@ -843,6 +965,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
         DeviceCtx& d = ctx->devs[di];
         if (di < BM_MAX_STAT_DEVICES) {
             st.dev_nonces[di] = d.piece_nonces;
+            if (ctx->timing || ctx->balance) st.dev_start_ms[di] = start_ms[di];
             float ms = 0.f;
             if ((ctx->timing || ctx->balance) && hipSetDevice(d.id) == hipSuccess &&
                 hipEventElapsedTime(&ms, d.bal[0], d.bal[1]) == hipSuccess)
@@ -870,6 +993,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
             ++li;
         }
     }
+    stamp_common(ctx);
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     out->hash = best.hash;
     out->nonce = best.nonce;
@@ -1081,6 +1205,9 @@ int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     const int dev = d.id, world = ctx->world, rank = ctx->rank;
+    // one deadline for the whole call: the wait for a pending join and the
+    // new join share timeout_ms
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
     // An earlier join this context gave up on may still be inside RCCL: wait
     // for it (within this call's timeout) rather than put a second worker
     // there; it has abandoned = true, so it aborts whatever it ends with.
@@ -1088,8 +1215,7 @@ int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
         auto& pj = ctx->pending_join;
         std::unique_lock<std::mutex> lk(pj->m);
         const bool ended = timeout_ms == 0 ? (pj->cv.wait(lk, [&] { return pj->done; }), true)
-                                           : pj->cv.wait_for(lk, std::chrono::milliseconds(timeout_ms),
-                                                             [&] { return pj->done; });
+                                           : pj->cv.wait_until(lk, deadline, [&] { return pj->done; });
         lk.unlock();
         if (!ended) {
             bm::trace("rank %d: the previous join is still inside RCCL; not starting another", rank);
@@ -1097,6 +1223,10 @@ int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
         }
         ctx->pending_worker.join();
         ctx->pending_join.reset();
+        if (timeout_ms > 0 && std::chrono::steady_clock::now() >= deadline) {
+            bm::trace("rank %d: the previous join ended, but no time is left for a new one", rank);
+            return BM_ETIMEDOUT;
+        }
     }
     // The join runs on a worker thread: a non-blocking ncclCommInitRankConfig
     // polled until it settles.  With a timeout the caller waits at most that
@@ -1109,7 +1239,7 @@ int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
     std::unique_lock<std::mutex> lk(job->m);
     if (timeout_ms == 0) {
         job->cv.wait(lk, [&] { return job->done; });
-    } else if (!job->cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return job->done; })) {
+    } else if (!job->cv.wait_until(lk, deadline, [&] { return job->done; })) {
         job->abandoned = true;
         lk.unlock();
         ctx->pending_join = job;
@@ -1122,6 +1252,7 @@ int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms) {
     bm::trace("rank %d: join status %d", rank, job->rc);
     if (job->rc != BM_OK) return job->rc;
     d.comm = job->comm;
+    ctx->rccl_init_ms = job->init_ms;
     ctx->joined = true;
     ctx->group_status = BM_OK;
     return BM_OK;
@@ -1237,6 +1368,12 @@ int bm_reduce_gpu(bm_ctx_t* ctx, const bm_result_t* parts, size_t n, bm_result_t
 int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches) {
     if (!ctx || launches < -1) return BM_EINVAL;
     ctx->fault_after = launches;
+    return BM_OK;
+}
+
+int bm_ctx_set_test_start_delay(bm_ctx_t* ctx, int device, int delay_us) {
+    if (!ctx || device < 0 || device >= (int)ctx->devs.size() || delay_us < 0) return BM_EINVAL;
+    ctx->devs[(size_t)device].test_delay_us = delay_us;
     return BM_OK;
 }
 

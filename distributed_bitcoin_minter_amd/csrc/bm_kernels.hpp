@@ -362,16 +362,19 @@ constexpr int kClockSlot = 16;
 #define BM_KATTR __attribute__((amdgpu_waves_per_eu(search_waves(P, NBV), 8)))
 #endif
 
-// PADC (the padding-block layouts of a one-block message): the IV and the
-// padding block's K + W are compile-time constants instead of kernargs
-// (kPadKW; the launcher checks the segment's mid / pad_w against them).
-template <int P, int NBV, bool PADC>
+// PADK >= 0 (the padding-block layouts of a message of PADK whole blocks
+// plus the varying one): the padding block's K + W are compile-time
+// constants instead of 64 kernargs (kPadKW<P, PADK>; the launcher checks the
+// segment's pad_w against them), and for PADK = 0 the entering state is the
+// IV, also folded.  PADK = -1: the generic kernel, everything from kernargs.
+template <int P, int NBV, int PADK>
 BM_DEV void search_body(const SearchArgs& A, Partial* __restrict__ part, unsigned long long* __restrict__ counter) {
     static_assert(P >= 0 && P < 64 && (NBV == 1 || (NBV == 2 && P <= 18)), "layout");
     constexpr int LW = P / 4;                      // last-block word holding the last digit
     constexpr int BOFF = 16 * (NBV - 1);           // word offset of the last block
     constexpr bool PADB = (NBV == 1) && (P >= 55); // a constant padding block follows
-    static_assert(!PADC || PADB, "PADC is a padding-block layout");
+    constexpr bool PADC = PADK >= 0;               // its constants folded
+    static_assert(!PADC || (PADB && PADK <= kMaxPadPrefixBlocks), "PADK is a padding-block layout");
     // Word LW holds only the last digit (P%4 == 0): a task's second digit is
     // stepped by an outer loop in word LW-1 (round LW-1 redone per step), so
     // tasks stay 100 nonces long instead of 10.
@@ -437,7 +440,7 @@ BM_DEV void search_body(const SearchArgs& A, Partial* __restrict__ part, unsigne
 
             uint32_t st[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) st[q] = PADC ? kIV256[q] : A.mid[q];
+            for (int q = 0; q < 8; ++q) st[q] = PADK == 0 ? kIV256[q] : A.mid[q];
             if constexpr (NBV == 2) {
                 uint32_t wa[16];
 #pragma unroll
@@ -511,7 +514,7 @@ BM_DEV void search_body(const SearchArgs& A, Partial* __restrict__ part, unsigne
                         static_for<0, 64>([&](auto I) {
                             constexpr int tt2 = decltype(I)::value;
                             if constexpr (PADC) {
-                                constexpr uint32_t kw = kPadKW<P>.v[tt2];
+                                constexpr uint32_t kw = kPadKW<P, (PADK > 0 ? PADK : 0)>.v[tt2];
                                 sha_round_kw<tt2>(z, kw);
                             } else {
                                 sha_round_kw<tt2, true>(z, A.padkw[tt2]);
@@ -576,17 +579,30 @@ BM_DEV void search_body(const SearchArgs& A, Partial* __restrict__ part, unsigne
 template <int P, int NBV>
 __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel(
     const SearchArgs A, Partial* __restrict__ part, unsigned long long* __restrict__ counter) {
-    search_body<P, NBV, false>(A, part, counter);
+    search_body<P, NBV, -1>(A, part, counter);
 }
 
 // The padding-block layouts (P >= 55) of a one-block message, with their
-// constants folded (search_body's PADC); NBV is 1 (a parameter only so the
-// occupancy attribute reads as for search_kernel).
+// constants folded (search_body's PADK = 0: IV and padding K + W); NBV is 1
+// (a parameter only so the occupancy attribute reads as for search_kernel).
 template <int P, int NBV = 1>
 __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel_padc(
     const SearchArgs A, Partial* __restrict__ part, unsigned long long* __restrict__ counter) {
     static_assert(NBV == 1 && P >= 55, "padding-block layouts only");
-    search_body<P, 1, true>(A, part, counter);
+    search_body<P, 1, 0>(A, part, counter);
+}
+
+// The same after K = 1 or 2 whole prefix blocks (messages whose "msg nonce"
+// ends at byte 64K + P, P >= 55: L + D between about 119 and 191): the
+// midstate comes from kernargs, the padding block's K + W are literals
+// (W15 = 8 * (64K + P + 1)), so the 64 kernarg words the generic kernel
+// keeps in SGPRs -- more than the file holds at this occupancy, hence its
+// v_readlane refills in the inner loop -- are gone.
+template <int P, int K, int NBV = 1>
+__global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel_padk(
+    const SearchArgs A, Partial* __restrict__ part, unsigned long long* __restrict__ counter) {
+    static_assert(NBV == 1 && P >= 55 && K >= 1 && K <= kMaxPadPrefixBlocks, "padding-block layouts only");
+    search_body<P, 1, K>(A, part, counter);
 }
 
 }  // namespace bm

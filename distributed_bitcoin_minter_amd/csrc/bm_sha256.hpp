@@ -28,21 +28,22 @@ constexpr uint32_t kK256[64] = {
 constexpr uint32_t kIV256[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
 
-// K[t] + W[t] of the constant padding block that follows a ONE-block
-// message whose last byte is at P >= 55 (no prefix block, so the state
-// entering the varying block is the IV): W0 = 0x80000000 when P = 63 (the
-// 0x80 byte spilled over), W15 = the message length in bits, W1..W14 = 0,
-// W16..W63 expanded at compile time.  The PADC kernels (bm_kernels.hpp) use
-// these as literal operands: no kernarg SGPRs, so their adds stay in the
-// fast class; the launcher checks a segment against them at run time.
+// K[t] + W[t] of the constant padding block that follows a message of K
+// whole 64-byte blocks plus a last block whose last byte is at P >= 55:
+// W0 = 0x80000000 when P = 63 (the 0x80 byte spilled over), W15 = the
+// message length in bits, 8 * (64K + P + 1), W1..W14 = 0, W16..W63 expanded
+// at compile time.  The folded padding-block kernels (bm_kernels.hpp:
+// search_kernel_padc, K = 0, whose entering state is the IV; search_kernel_padk,
+// K = 1 or 2, after a midstate) use these as literal operands instead of 64
+// kernarg SGPRs; the launcher checks a segment against them at run time.
 struct KW64 {
     uint32_t v[64];
 };
 constexpr uint32_t crotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
-constexpr KW64 pad_kw_const(int P) {
+constexpr KW64 pad_kw_const(int P, int K = 0) {
     uint32_t w[64] = {};
     w[0] = P == 63 ? 0x80000000u : 0u;
-    w[15] = 8u * (uint32_t)(P + 1);
+    w[15] = 8u * (uint32_t)(64 * K + P + 1);
     for (int t = 16; t < 64; ++t) {
         const uint32_t x = w[t - 15], y = w[t - 2];
         w[t] = (crotr(y, 17) ^ crotr(y, 19) ^ (y >> 10)) + w[t - 7] + (crotr(x, 7) ^ crotr(x, 18) ^ (x >> 3)) +
@@ -52,8 +53,9 @@ constexpr KW64 pad_kw_const(int P) {
     for (int t = 0; t < 64; ++t) r.v[t] = kK256[t] + w[t];
     return r;
 }
-template <int P>
-inline constexpr KW64 kPadKW = pad_kw_const(P);
+template <int P, int K = 0>
+inline constexpr KW64 kPadKW = pad_kw_const(P, K);
+constexpr int kMaxPadPrefixBlocks = 2;  // search_kernel_padk<P, K>: K = 1..2 prefix blocks
 
 namespace host {
 

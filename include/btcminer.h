@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BM_ABI_VERSION 6
+#define BM_ABI_VERSION 7
 
 /* status codes */
 #define BM_OK 0
@@ -82,8 +82,8 @@ int bm_device_pci_bus_id(int device, char* buf, int len);
  * default 2); BTCMINER_TAIL = nonces split off the biggest launch into a
  * short-task launch of their own (default 16777216, 0 = off); BTCMINER_CHUNK =
  * nonces per lane per work-counter dequeue, at most (10..100000, default 100);
- * BTCMINER_PADC=0 = never use the padding-block kernel with folded constants
- * (search_kernel_padc; default: wherever it applies). */
+ * BTCMINER_PADC=0 = never use the padding-block kernels with folded constants
+ * (search_kernel_padc / search_kernel_padk; default: wherever they apply). */
 int bm_ctx_create(int num_gpus, bm_ctx_t** out);
 /* Context over an explicit device list (e.g. {LOCAL_RANK} for one process
  * per GPU).  A device listed twice is allowed (a one-GPU rehearsal of the
@@ -126,15 +126,20 @@ int bm_ctx_create_devices(const int* devices, int n, bm_ctx_t** out);
  *      communicator error or wait for their peer timeout.
  * bm_ctx_create_rank() is both steps in one call (blocking join).
  * bm_ctx_set_peer_timeout(): a joined rank waits at most this long for the
- *   group's allgather after its own work ends (0, the default: no limit);
- *   past it the communicator is aborted and the call returns BM_ETIMEDOUT,
- *   as does every later search until bm_ctx_leave_rank().
+ *   group's allgather after its own work ends (default BM_DEFAULT_PEER_TIMEOUT_MS,
+ *   10 minutes, so a peer that never posts its slot is a bounded failure;
+ *   0: no limit); past it the communicator is aborted and the call returns
+ *   BM_ETIMEDOUT, as does every later search until bm_ctx_leave_rank().
+ *   Callers whose pieces take longer than that per call raise it.
+ * bm_ctx_join_rank(): timeout_ms bounds the WHOLE call, including the wait
+ *   for a pending join; 0 waits without limit.
  * bm_ctx_leave_rank(): drop the communicator; searches return the rank's
  *   own partial again.  bm_ctx_rank_joined(): 1 inside a group, else 0.
  * bm_ctx_destroy() (any context) waits for its own streams, then drops every
  *   communicator it holds with ncclCommAbort: teardown never waits on a peer,
  *   even one that has died. */
 #define BM_RCCL_ID_BYTES 128
+#define BM_DEFAULT_PEER_TIMEOUT_MS 600000
 int bm_rccl_unique_id(uint8_t* id /* BM_RCCL_ID_BYTES */);
 int bm_ctx_create_rank_local(int device, int rank, int world, bm_ctx_t** out);
 int bm_ctx_join_rank(bm_ctx_t* ctx, const uint8_t* id, int timeout_ms);
@@ -164,8 +169,11 @@ typedef struct bm_launch_stat {
     int32_t device;       /* index into the context's device list */
     int32_t p;            /* byte position of the last digit in its SHA block */
     int32_t nbv;          /* varying blocks per task (1 or 2) */
-    int32_t pad_block;    /* 1 when a constant padding block follows; 2: the same, run by the
-                             kernel with that block's constants folded in (a one-block message) */
+    int32_t pad_block;    /* 1 when a constant padding block follows (the generic kernel: its
+                             K + W from kernargs); 2 + K: the same, run by a kernel with that
+                             block's constants folded in, after K whole prefix blocks (2: a
+                             one-block message, search_kernel_padc; 3, 4: K = 1, 2,
+                             search_kernel_padk, whose entering state is the midstate) */
     int32_t digits;       /* decimal digits of every nonce in the launch */
     int32_t inner_digits; /* digits iterated by each thread's inner loop */
     uint64_t nonces;      /* nonces the launch is responsible for */
@@ -210,6 +218,27 @@ typedef struct bm_stats {
     int32_t dev_rccl_rank[BM_MAX_STAT_DEVICES];   /* ncclCommUserRank of each device of the context */
     int32_t dev_rccl_device[BM_MAX_STAT_DEVICES]; /* ncclCommCuDevice: the HIP device RCCL runs that
                                                      rank on */
+    /* ABI 7: what the combine and the start of a call cost, so a multi-GPU
+     * line can be read without a rerun. */
+    int32_t rccl_version;      /* ncclGetVersion of the RCCL the library runs on (e.g. 22703); 0 if
+                                  it cannot say.  Filled on every call. */
+    int32_t start_threads;     /* host threads that submitted the devices' work (1, or one per
+                                  device of a multi-device context) */
+    double rccl_init_ms;       /* host time the current communicator took to form: ncclCommInitAll
+                                  (one process), or bm_ctx_join_rank's init, which includes waiting
+                                  for every rank to arrive; 0 without a communicator */
+    double rccl_allgather_ms;  /* the last call's allgather, from HIP events around it on the
+                                  (first) device's stream (timing on): it starts when this
+                                  device's own work is done, so it includes the wait for the
+                                  slowest peer; max over the devices of a context; 0 otherwise */
+    double combine_ms;         /* host wall time of the call's combine stage (allgather or host
+                                  copies, and the final stream synchronisations) */
+    double dev_allgather_ms[BM_MAX_STAT_DEVICES]; /* each device's allgather event pair (timing on) */
+    double dev_start_ms[BM_MAX_STAT_DEVICES];     /* host time at which each device's first
+                                  operation of the call was submitted, relative to the earliest
+                                  device's (its stream is idle then, so this is when it starts);
+                                  set_balance measures rates from that common start (timing or
+                                  balance on) */
     bm_launch_stat_t launch[BM_MAX_LAUNCH_STATS];
 } bm_stats_t;
 
@@ -265,8 +294,11 @@ int bm_ctx_set_combine(bm_ctx_t* ctx, int mode);
  *   rank of a group must set the same shares.  n = 0: back to near-equal.
  * bm_ctx_set_balance: a multi-device context sets its own shares after each
  *   search in which every device's piece held >= 2^30 nonces: each device's
- *   nonces over the time from its first operation to its reduction, scaled so
- *   the fastest device has 65536.  BM_EINVAL on a rank context of more than
+ *   nonces over the time from the call's common start (the earliest device's
+ *   first operation; bm_stats_t.dev_start_ms) to its reduction, scaled so the
+ *   fastest device has 65536 -- a device that starts late gets a smaller
+ *   piece.  Each device's work is submitted from a host thread of its own, so
+ *   the starts are close anyway.  BM_EINVAL on a rank context of more than
  *   one rank: a rank sees only its own device, so a group exchanges its rates
  *   itself and calls bm_ctx_set_split (bench.py does, over its rendezvous).
  * bm_ctx_get_split: the shares the next search will use (*n = 0: near-equal).
@@ -303,6 +335,11 @@ int bm_ctx_set_test_fault(bm_ctx_t* ctx, int launches);
  * allgather succeeds but its last slot carries a failure status, as a failed
  * peer's slot does: the call returns BM_EPEER and the group stays joined. */
 int bm_ctx_set_test_rccl_fault(bm_ctx_t* ctx, int where);
+
+/* Hold back the submission of device `device`'s work (an index into the
+ * context's device list) by delay_us microseconds at the start of every later
+ * search (0: off): a late-starting GPU, on demand, for the balance test. */
+int bm_ctx_set_test_start_delay(bm_ctx_t* ctx, int device, int delay_us);
 
 /* ---- host-side plan introspection (pure CPU; used by the CPU tests) ---- */
 

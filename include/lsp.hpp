@@ -603,6 +603,14 @@ class Server {
         drop_if_done(conn_id);
     }
 
+    // True when every connection's written messages have all been
+    // acknowledged (none waiting for the window, none in flight): what a
+    // caller checks before it lets its clients go.
+    bool Drained() {
+        std::lock_guard<std::mutex> g(mu_);
+        return std::all_of(conns_.begin(), conns_.end(), [](const auto& kv) { return kv.second->ep.drained(); });
+    }
+
     // Blocks until every client's pending messages are acknowledged or that
     // client is lost; ServerError(0) if any was lost meanwhile.
     void Close() {

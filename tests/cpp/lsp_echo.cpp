@@ -1,11 +1,14 @@
 // lsp_echo.cpp -- test driver for lsp::Server (include/lsp.hpp): echoes every
 // payload back to the connection it came from.  Prints "port <n>" first; on
 // stdin EOF it calls Close() and prints "closed ok" or "closed lost".  Lost
-// connections are reported as "lost <id>".  Built and run by
+// connections are reported as "lost <id>".  A stdin line "drain" waits (at
+// most 60 s) until every echo written so far is acknowledged and prints
+// "drained" (or "not drained").  Built and run by
 // tests/test_cpp_server.py (the Python LSP clients are the other side).
 //
 //   lsp_echo [--epoch-limit K] [--epoch-millis MS] [--window-size W]
 //            [--drop-read P] [--drop-write P]
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
@@ -46,6 +49,12 @@ int main(int argc, char** argv) {
     });
     std::string line;
     while (std::getline(std::cin, line)) {
+        if (line != "drain") continue;
+        bool ok = false;
+        for (int i = 0; i < 12000 && !(ok = srv->Drained()); ++i)
+            std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        std::printf(ok ? "drained\n" : "not drained\n");
+        std::fflush(stdout);
     }
     bool lost = false;
     try {

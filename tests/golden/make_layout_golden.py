@@ -11,10 +11,13 @@ re-computed with hashlib (an independent SHA-256).
 Messages are L bytes 'a'.. (tools/len_sweep.py's); lengths:
   50  last digit at byte 60 of block 0: padding block, search_kernel_padc
   46  byte 56 of block 0 (P % 4 = 0): padc with the two-word inner loop
-  114 byte 60 of block 1: padding block after a prefix block, the generic kernel
+  114 byte 60 of block 1: padding block after a prefix block (the generic kernel
+      until round 4; search_kernel_padk<60, 1> since round 5)
+  178 byte 60 of block 2: padding block after two prefix blocks, search_kernel_padk<60, 2>
   59  digits straddle blocks 0 and 1: NBV = 2
 
-Usage: python tests/golden/make_layout_golden.py [--threads T]   (about a minute per length on 8 cores)
+Usage: python tests/golden/make_layout_golden.py [--threads T] [--lengths 178 ...]
+       (about a minute per length on 8 cores; --lengths recomputes only those and keeps the others)
 """
 import argparse
 import hashlib
@@ -26,7 +29,8 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 CLI = os.path.join(ROOT, "oracle", "oracle_cli")
-LENGTHS = {50: "padc", 46: "padc, two-word inner loop", 114: "generic padding block", 59: "NBV = 2"}
+LENGTHS = {50: "padc", 46: "padc, two-word inner loop", 114: "padding block after one prefix block",
+           59: "NBV = 2", 178: "padding block after two prefix blocks"}
 LO = 10 ** 9
 HI = LO + (1 << 32) - 1
 
@@ -48,10 +52,16 @@ def scan(kind, msg, lo, hi, threads):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
+    ap.add_argument("--lengths", type=int, nargs="*", default=None)
     a = ap.parse_args()
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    path = os.path.join(HERE, "layout_ranges.json")
+    old = {c["len"]: c for c in json.load(open(path))["cases"]} if a.lengths and os.path.exists(path) else {}
     cases = []
     for L, what in LENGTHS.items():
+        if a.lengths and L not in a.lengths and L in old:
+            cases.append(dict(old[L], layout=what))
+            continue
         msg = message(L)
         w = (HI - (1 << 21) + 1, HI)
         assert scan("search16", msg, *w, a.threads) == scan("search", msg, *w, a.threads), L
@@ -60,7 +70,7 @@ def main():
         assert ref_hash(msg, n) == h and LO <= n <= HI, L
         cases.append({"len": L, "layout": what, "msg_hex": msg.hex(), "lower": LO, "upper": HI, "hash": h, "nonce": n})
         print(L, what, h, n, f"{time.time() - t:.0f} s", flush=True)
-    with open(os.path.join(HERE, "layout_ranges.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump({"generator": "oracle/oracle_cli search16 (AVX-512), checked against the OpenSSL loop on a "
                                 "2^21 window per message; answers re-hashed with hashlib", "cases": cases}, f, indent=0)
         f.write("\n")

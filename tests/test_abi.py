@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     lib = _lib.load()
-    assert lib.bm_abi_version() == _lib.BM_ABI_VERSION == 6
+    assert lib.bm_abi_version() == _lib.BM_ABI_VERSION == 7
     for code in range(0, -9, -1):
         assert lib.bm_strerror(code).decode() != "unknown status"
     assert lib.bm_strerror(-99).decode() == "unknown status"
@@ -60,6 +60,7 @@ def test_invalid_arguments_rejected():
     assert lib.bm_ctx_set_peer_timeout(None, 10) == _lib.BM_EINVAL
     assert lib.bm_ctx_set_test_rccl_fault(None, 1) == _lib.BM_EINVAL
     assert lib.bm_ctx_set_test_rccl_fault(None, 3) == _lib.BM_EINVAL
+    assert lib.bm_ctx_set_test_start_delay(None, 0, 10) == _lib.BM_EINVAL
     assert lib.bm_reduce_gpu(None, None, 0, ctypes.byref(r)) == _lib.BM_EINVAL
     assert lib.bm_ctx_set_test_fault(None, 0) == _lib.BM_EINVAL
     assert lib.bm_ctx_rank(None, ctypes.byref(n), ctypes.byref(n)) == _lib.BM_EINVAL
@@ -194,6 +195,21 @@ def test_miner_patch_applies_to_the_reference():
     assert "bitcoin.Hash(" not in got.split("func workWorkWorkWorkWork")[1].split("\n}\n")[0]
     assert "min_hash, min_nonce, scan_err := scan(job_msg.Data, job_msg.Lower, job_msg.Upper)" in got
     assert "result := bitcoin.NewResult(min_hash, min_nonce)" in got
+    # the patch also removes what kept the file itself from compiling
+    assert "string hostport" not in got and "hostport := os.Args[1]" in got            # :26
+    assert "bitcoin.NewRequest{}" not in got and "job_msg := bitcoin.Message{}" in got  # :54
+    assert "var miner lsp.Client" in got and "var miner_err error" in got              # :30
+    imports = got.split("import (")[1].split(")")[0]
+    assert '"log"' in imports and '"errors"' not in imports and "lspnet" not in imports  # :92, :5, :8
+    assert "_, write_msg_err :=" not in got  # lsp.Client.Write returns one value
+
+
+def test_peer_timeout_default_is_bounded():
+    """a joined rank's default wait for its peers is finite, and
+    the binding's constant is the header's."""
+    src = open(os.path.join(ROOT, "include", "btcminer.h")).read()
+    m = re.search(r"#define BM_DEFAULT_PEER_TIMEOUT_MS (\d+)", src)
+    assert m and int(m.group(1)) == _lib.BM_DEFAULT_PEER_TIMEOUT_MS > 0
 
 
 def _c_client(tmp):

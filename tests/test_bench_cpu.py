@@ -122,7 +122,11 @@ class FakeCtx:
             nonces=n, span_ms=1.0, combine_used=_lib.BM_COMBINED_RCCL if j else _lib.BM_COMBINED_LOCAL,
             rccl_status=0, rccl_nranks=self.world_ if j else 0, rccl_rank=self.rank_ if j else -1, devices=1,
             dev_nonces=[n], dev_span_ms=[1.0], dev_rccl_rank=[self.rank_ if j else -1],
-            dev_rccl_device=[0 if j else -1])
+            dev_rccl_device=[0 if j else -1],
+            # ABI 7: what the library reports of RCCL -- nothing without a group
+            rccl_version=22703, rccl_init_ms=40.0 + self.rank_ if j else 0.0,
+            rccl_allgather_ms=0.05 + 0.01 * self.rank_ if j else 0.0, combine_ms=0.2 if j else 0.01,
+            start_threads=1, dev_start_ms=[0.0], dev_allgather_ms=[0.05 + 0.01 * self.rank_ if j else 0.0])
 
 bench.Context = FakeCtx
 bench.device_count = lambda: 1
@@ -134,11 +138,13 @@ world = int(os.environ["WORLD_SIZE"])
 ctx, grp, search, how, dev = bench.open_contexts(args, world, int(os.environ["RANK"]), int(os.environ["LOCAL_RANK"]))
 res = search(b"bradfitz", 0, 99_999)
 # the line's per-rank summaries and its validity, as main() builds them
-slots = grp.gather(bench.rank_summary(grp.rank, dev, [bench.step_record(ctx.last_stats())], None))
+rec = bench.step_record(ctx.last_stats())
+slots = grp.gather(bench.rank_summary(grp.rank, dev, [rec], None, 0.0))
 valid = bench.scaling_validity(world, slots, args.combine, False)
+costs = bench.rccl_costs(slots, rec["rccl_version"])
 grp.close()
 print(json.dumps({"rank": grp.rank, "how": how, "dev": dev, "joined": ctx.joined(), "res": list(res),
-                  "slots": slots, "valid": valid}))
+                  "slots": slots, "valid": valid, "costs": costs}))
 """
 
 
@@ -175,6 +181,12 @@ def test_bench_ranks_join_together(oracle):
         assert [s["rccl_rank"] for s in r["slots"]] == [0, 1, 2]
         assert len({s["pci_bus_id"] for s in r["slots"]}) == 3
         assert r["valid"] == {"scaling_valid": True}, r["valid"]
+        # the line's RCCL costs -- version, the slowest init, the
+        # allgather's event pair (min / max over ranks), the combine's host time
+        c = r["costs"]["rccl"]
+        assert (c["version"], c["version_str"], c["init_ms"]) == (22703, "2.27.3", 42.0), c
+        assert (c["allgather_ms_min"], c["allgather_ms_max"]) == (0.05, 0.07) and c["combine_ms_max"] == 0.2, c
+        assert [s["allgather_ms"] for s in r["slots"]] == [0.05, 0.06, 0.07]
 
 
 def test_bench_ranks_fall_back_together_when_one_join_fails(oracle):
@@ -192,6 +204,9 @@ def test_bench_ranks_fall_back_together_when_one_join_fails(oracle):
         assert r["valid"]["scaling_valid"] is False
         assert any("instead of one RCCL allgather" in w for w in r["valid"]["scaling_invalid"]), r["valid"]
         assert all(s["rccl_nranks"] == 0 and s["combine"] == "local" for s in r["slots"])
+        # the rendezvous path ran no RCCL collective: no RCCL costs, and the reason
+        assert r["costs"] == {"rccl": None, "rccl_absent": "combine local: no RCCL collective ran"}, r["costs"]
+        assert all(s["allgather_ms"] == 0 and s["rccl_init_ms"] == 0 for s in r["slots"])
     outs = _rank_setup(2, COMBINE="gather")
     res = [json.loads(o.strip().splitlines()[-1]) for rc, o, e in outs if rc == 0]
     assert len(res) == 2 and all("--combine gather" in r["how"] and r["res"] == want for r in res)
@@ -294,3 +309,23 @@ def test_one_process_device_summaries(monkeypatch):
     slots = bench.device_summaries([bench.step_record(stats(_lib.BM_COMBINED_HOST, 0))], [0, 1, 2, 3])
     v = bench.scaling_validity(4, slots, "rccl", False)
     assert v["scaling_valid"] is False and "combine host" in v["scaling_invalid"][0]
+
+
+def test_kernel_names_and_isa_keys():
+    """The launch stats' pad_block names the kernel rocprof prints and its
+    isa_mix.json entry: 2 = search_kernel_padc<P, 1>, 2 + K =
+    search_kernel_padk<P, K, 1>, and every padk layout has a
+    static count there with no more issue slots than the generic kernel's."""
+    import json
+    assert bench.kernel_name(18, 1) == "search_kernel<18, 1>" and bench.isa_key(18, 1) == "18:1"
+    assert bench.kernel_name(60, 1, 2) == "search_kernel_padc<60, 1>" and bench.isa_key(60, 1, 2) == "60:c"
+    assert bench.kernel_name(60, 1, 4) == "search_kernel_padk<60, 2, 1>" and bench.isa_key(60, 1, 4) == "60:k2"
+    lay = json.load(open(os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc", "isa_mix.json")))["layouts"]
+    for p in range(55, 64):
+        for k in (1, 2):
+            assert lay[f"{p}:k{k}"]["issue_slots"] <= lay[f"{p}:1"]["issue_slots"], (p, k)
+    assert bench.issue_bound("60:k1", 2.4)["GHs_per_gpu"] > bench.issue_bound("60:1", 2.4)["GHs_per_gpu"]
+
+
+def test_rccl_version_str():
+    assert bench.rccl_version_str(22703) == "2.27.3" and bench.rccl_version_str(0) is None

@@ -18,7 +18,6 @@ race (TSan prints "WARNING: ThreadSanitizer" and, with halt_on_error, exits
 import os
 import subprocess
 import threading
-import time
 
 import pytest
 
@@ -112,10 +111,13 @@ def test_echo_concurrent_clients_under_drops(tsan, tmp_path):
         for echoed, sent in got.values():
             assert echoed == sent  # in order, exactly once
         lspnet.ResetDropPercent()
-        # the server still drops 20% of what it reads: give its resends of the
-        # last echoes some epochs to be acked before the clients go, or a
-        # loaded host can leave one unacked and the server declares it lost
-        time.sleep(0.5)
+        # the server still drops 20% of what it reads, so acks of its last
+        # echoes can be lost and those echoes resent: the clients go only once
+        # the server says every echo is acknowledged (a condition,
+        # not a fixed sleep), so Close() has nothing left to wait for
+        srv.p.stdin.write("drain\n")
+        srv.p.stdin.flush()
+        assert srv.p.stdout.readline().strip() == "drained", srv.report()
         for c in clients:
             c.Close()
         assert srv.finish().splitlines()[-1] == "closed ok"

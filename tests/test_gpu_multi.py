@@ -237,13 +237,25 @@ def test_bench_one_process_rehearsal():
     assert out["n_gpus"] == 2 and out["config"]["global_nonces"] == 2 ** 33
     assert out["result_ok"] in (True, None) and "rehearsal" in out
     assert out["scaling_valid"] is False and "rehearsal" in out["scaling_invalid"][0]
+    # every line carries north_star's 2^40 target, one warm C4 step
+    # split over the N slots, checked against the 2^40 golden
+    c4 = out["c4"]
+    assert (c4["lower"], c4["upper"], c4["nonces"], c4["scaling"]) == (0, 2 ** 40 - 1, 2 ** 40, "strong"), c4
+    assert c4["result_ok"] is True and c4["result"] == c4["golden"] == [16555811, 890536971553], c4
+    assert len(c4["devices"]) == 2 and sum(d["nonces"] for d in c4["devices"]) == 2 ** 40, c4
+    assert c4["combine"] == "host" and c4["GHs"] > 10 and c4["seconds"] > 1, c4
+    # the one-process line reports the start of each device's work (a host
+    # thread per device) and, with no RCCL combine, why there is no RCCL block
+    assert out["start_threads"] == 2 and out["start_skew_ms"] >= 0, out
+    assert out["rccl"] is None and "no RCCL collective ran" in out["rccl_absent"], out
 
 
 def test_bench_torchrun_rehearsal():
     """bench.py under torchrun with 2 ranks on GPU 0 (file rendezvous,
     gather of the partials); the GPU processes map one HIP runtime."""
-    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--rehearse-one-gpu"], torchrun=2))
+    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--rehearse-one-gpu", "--no-c4"], torchrun=2))
     assert out["n_gpus"] == 2 and out["result_ok"] in (True, None)
+    assert out["start_skew_ms"] >= 0 and all("start_offset_ms" in r for r in out["config"]["ranks"]), out
     assert len(out["hip_runtime"]) == 1, out["hip_runtime"]
     assert out["scaling_valid"] is False and "rehearsal" in out["scaling_invalid"][0]
 
@@ -254,10 +266,19 @@ def test_bench_torchrun_rccl_world1():
     WORLD_SIZE is forced to 1 by the launcher: covered by
     test_rank_context_world1.  Here: the N = 1 line is well formed and maps
     one HIP runtime."""
-    out = _line(_bench(["--gpus", "1", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]))
-    assert out["result_ok"] is True and out["n_gpus"] == 1
+    out = _line(_bench(["--gpus", "1", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-c4"]))
+    assert out["result_ok"] is True and out["n_gpus"] == 1 and "c4" not in out
     assert len(out["hip_runtime"]) == 1 and "/opt/rocm" in out["hip_runtime"][0]
     assert out["roofline"]["frac"] > 0.5
+    # VERDICT r4: the PMC figures are the committed pass's, marked as imported
+    roof = out["roofline"]
+    pm = roof["pmc"]
+    assert pm["imported"] is True and pm["src"].startswith("profiles/") and pm["box_clock_ghz"] > 1.0, pm
+    assert pm["valu_per_nonce"] > 1000 and 0.5 < pm["valu_dual_issued_frac"] <= 1.0, pm
+    assert roof["traffic"] == pm["hbm_bytes_per_launch"] and roof["traffic_imported"] is True
+    for k in ("valu_per_nonce_pmc", "valu_dual_issued_frac_pmc", "clock_ghz_pmc"):
+        assert k not in roof, k
+    assert "imported" in roof["executed"]["src"], roof["executed"]
     ex = out["roofline"]["executed"]  # VERDICT r3: executed VALU lane-ops, always below the peak
     assert ex and 0.5 < ex["frac"] < 1.0 and ex["valu_per_nonce"] > 1000, ex
     assert "ceiling" in out["roofline"]["issue_bound"]["role"]
@@ -458,10 +479,12 @@ def test_bench_rehearsals_balance_after_warmup():
     and 2 torchrun ranks exchange the rates of their second (warm) warmup step
     over the rendezvous and cut by the shares (dist.rank_piece); both
     answers equal the weak2 golden."""
-    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--rehearse-one-gpu"]))
+    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--rehearse-one-gpu",
+                        "--no-c4"]))
     sp = out["config"]["split"]
     assert out["result_ok"] is True and sp["mode"].startswith("measured device rates") and len(sp["shares"]) == 2
-    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "2", "--rehearse-one-gpu"], torchrun=2))
+    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "2", "--rehearse-one-gpu", "--no-c4"],
+                       torchrun=2))
     sp = out["config"]["split"]
     assert out["result_ok"] is True and sp["mode"].startswith("measured rank rates"), sp
     assert len(sp["shares"]) == 2 and max(sp["shares"]) == 65536
@@ -484,19 +507,28 @@ def test_rccl_failure_falls_back_to_host_copies(oracle, where):
     want = oracle.search(msg, lo, hi, threads=8)
     with Context(devices=[0]) as c:
         c.set_combine(BM_COMBINE_RCCL)
+        c.set_timing(True)
         assert c.search(msg, lo, hi) == want
         st = c.last_stats()
         assert (st.combine_used, st.rccl_status) == (BM_COMBINED_RCCL, 0)
         # ncclCommInitAll over the context's one device: RCCL reports 1 rank, on device 0
         assert (st.rccl_nranks, st.rccl_rank, st.dev_rccl_rank[0], st.dev_rccl_device[0]) == (1, 0, 0, 0)
+        # VERDICT r4 (ABI 7): RCCL's version, the communicator's set-up time and
+        # the allgather's event pair, so a multi-GPU line reads without a rerun
+        assert st.rccl_version >= 20000 and st.rccl_init_ms > 0, (st.rccl_version, st.rccl_init_ms)
+        assert 0 < st.rccl_allgather_ms == st.dev_allgather_ms[0] < 1000 and st.combine_ms > 0
+        assert st.start_threads == 1 and st.dev_start_ms[0] == 0
     with Context(devices=[0]) as c:
         c.set_combine(BM_COMBINE_RCCL)
         c.set_test_rccl_fault(where)
+        c.set_timing(True)
         for _ in range(2):
             assert c.search(msg, lo, hi) == want
             st = c.last_stats()
             assert (st.combine_used, st.rccl_status) == (BM_COMBINED_HOST, BM_ERCCL)
             assert (st.rccl_nranks, st.rccl_rank) == (0, -1)
+            # no communicator left, no allgather: nothing of RCCL but its version
+            assert (st.rccl_init_ms, st.rccl_allgather_ms) == (0, 0) and st.rccl_version >= 20000
         c.set_test_rccl_fault(0)
         assert c.search(bytes.fromhex(C2["msg_hex"]), C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
         assert c.last_stats().combine_used == BM_COMBINED_HOST  # stays on host copies
@@ -556,9 +588,13 @@ def test_rank_group_world1_status_and_leave(oracle):
         c.join(rccl_unique_id(), timeout_ms=60_000)
         assert c.joined()
         c.set_peer_timeout(60_000)
+        c.set_timing(True)
         assert c.search(msg, lo, hi) == want and c.last_stats().combine_used == BM_COMBINED_RCCL
         st = c.last_stats()  # what RCCL itself says about the group
         assert (st.rccl_nranks, st.rccl_rank, st.dev_rccl_rank[0], st.dev_rccl_device[0]) == (1, 0, 0, 0)
+        # VERDICT r4 (ABI 7): the join's init time, RCCL's version, the allgather's event pair
+        assert st.rccl_version >= 20000 and st.rccl_init_ms > 0, (st.rccl_version, st.rccl_init_ms)
+        assert 0 < st.rccl_allgather_ms == st.dev_allgather_ms[0] < 1000 and st.combine_ms > 0, st.rccl_allgather_ms
         for fault in (0, 1):
             c.set_test_fault(fault)
             with pytest.raises(BtcMinerError) as ei:
@@ -587,6 +623,7 @@ def test_rank_group_world1_status_and_leave(oracle):
         assert c.search(msg, lo, hi) == want and c.last_stats().combine_used == BM_COMBINED_LOCAL
         st = c.last_stats()
         assert (st.rccl_nranks, st.rccl_rank, st.dev_rccl_rank[0], st.dev_rccl_device[0]) == (0, -1, -1, -1)
+        assert (st.rccl_init_ms, st.rccl_allgather_ms) == (0, 0)  # out of the group: no communicator
         c.join(rccl_unique_id())
         assert c.search(bytes.fromhex(C2["msg_hex"]), C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
         c.leave()
@@ -632,7 +669,7 @@ def test_bench_torchrun_with_per_rank_visibility_mask():
     line names that combine, and each rank's nonces, which add up to the
     workload; the answer equals the weak2 golden."""
     env = dict(os.environ, HIP_VISIBLE_DEVICES="0")
-    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], env=env, torchrun=2))
+    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-c4"], env=env, torchrun=2))
     assert out["result_ok"] is True and out["n_gpus"] == 2
     cfg = out["config"]
     assert "rendezvous gather" in cfg["parallelism"] and "RCCL group failed" in cfg["parallelism"], cfg
@@ -644,6 +681,9 @@ def test_bench_torchrun_with_per_rank_visibility_mask():
     why = " | ".join(out["scaling_invalid"])
     assert "instead of one RCCL allgather" in why and "1 distinct GPUs" in why, why
     assert len({r["pci_bus_id"] for r in ranks}) == 1 and all(r["rccl_nranks"] == 0 for r in ranks)
+    # nothing of RCCL ran, so the line has no RCCL costs, and says why
+    assert out["rccl"] is None and "combine local" in out["rccl_absent"], out
+    assert all(r["allgather_ms"] == 0 and r["rccl_init_ms"] == 0 for r in ranks), ranks
 
 
 def test_clock_probe_library():
@@ -660,3 +700,45 @@ def test_clock_probe_library():
         st = c.last_stats()
         dom = max((st.launch[i] for i in range(st.recorded)), key=lambda L: L.nonces)
         assert 1.0 < dom.clock_ghz < 3.0, dom.clock_ghz
+
+
+# ---- start skew and balance from a common start (ABI 7) ----------
+
+
+def test_start_skew_reported_on_eight_slots():
+    """A one-process context of 8 device slots (all GPU 0: a rehearsal of the
+    one-process 8-GPU design) submits each slot's work from a host thread of
+    its own and reports each slot's start against the earliest one
+    (bm_stats_t.dev_start_ms): 8 threads, the earliest at 0, all within a few
+    ms; the answer is C2's."""
+    msg = bytes.fromhex(C2["msg_hex"])
+    with Context(devices=[0] * 8) as c:
+        c.set_timing(True)
+        assert c.search(msg, C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
+        st = c.last_stats()
+        starts = [st.dev_start_ms[i] for i in range(8)]
+        assert st.start_threads == 8 and min(starts) == 0 and max(starts) < 50, starts
+        assert all(st.dev_nonces[i] > 0 for i in range(8))
+
+
+@pytest.mark.parametrize("late", [0, 1])
+def test_balance_reacts_to_start_delay(late):
+    """bm_ctx_set_balance measures each device's rate from the call's common
+    start: with one device's submission held back by 150 ms (test hook), that
+    device's share drops well below the other's, its dev_start_ms shows the
+    delay, and the answers stay C2's."""
+    msg = bytes.fromhex(C2["msg_hex"])
+    with Context(devices=[0, 0]) as c:
+        c.set_balance(True)
+        c.set_test_start_delay(late, 150_000)
+        assert c.search(msg, C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
+        st = c.last_stats()
+        assert st.dev_start_ms[late] >= 140 and st.dev_start_ms[1 - late] == 0, list(st.dev_start_ms[:2])
+        sh = c.get_split()
+        assert sh[1 - late] == 65536 and sh[late] < 0.75 * 65536, sh
+        with pytest.raises(BtcMinerError) as ei:
+            c.set_test_start_delay(2, 10)
+        assert ei.value.status == BM_EINVAL
+        c.set_test_start_delay(late, 0)
+        assert c.search(msg, C2["lower"], C2["upper"]) == (C2["hash"], C2["nonce"])
+        assert c.get_split()[late] > sh[late]  # no delay: its share grows back

@@ -129,8 +129,8 @@ def test_edges(gpu_ctx, oracle):
 
 @pytest.fixture(scope="module")
 def generic_pad_ctx():
-    """A context that never uses search_kernel_padc (BTCMINER_PADC=0, read at
-    creation): the generic padding-block kernel for every such layout."""
+    """A context that never uses search_kernel_padc / _padk (BTCMINER_PADC=0,
+    read at creation): the generic padding-block kernel for every such layout."""
     import os
     from distributed_bitcoin_minter_amd import Context
     old = os.environ.get("BTCMINER_PADC")
@@ -150,15 +150,18 @@ def generic_pad_ctx():
 def test_padding_block_layouts_folded_and_generic(gpu_ctx, generic_pad_ctx, oracle, P):
     """The padding-block layouts (last digit at byte P >= 55 of its block, so
     SHA-256's length words spill into a block of their own), 10-digit
-    nonces, both task shapes: a one-block message runs search_kernel_padc (IV
-    and padding constants folded; stats pad_block = 2), the same message
-    under BTCMINER_PADC=0 and a two-block message (prefix midstate) run the
-    generic kernel (pad_block = 1); every answer equals the oracle's."""
+    nonces, both task shapes: a message of K whole prefix blocks plus the
+    varying one runs the kernel with the padding block's constants folded --
+    K = 0: search_kernel_padc (IV folded too; stats pad_block = 2), K = 1, 2:
+    search_kernel_padk<P, K> (midstate from kernargs; pad_block = 3, 4,
+    VERDICT r4) -- and K = 3, or any K under BTCMINER_PADC=0, the generic
+    kernel (pad_block = 1); every answer equals the oracle's."""
     lo = 10 ** 9 + 7_777_777
     hi = lo + 20_000
-    one = bytes(97 + i % 26 for i in range(P - 10))        # L + 1 + 10 bytes end at byte P of block 0
-    two = bytes(65 + i % 26 for i in range(P - 10 + 64))   # ... of block 1
-    for ctx, msg, pad in ((gpu_ctx, one, 2), (generic_pad_ctx, one, 1), (gpu_ctx, two, 1)):
+    msgs = [bytes(97 + (i + k) % 26 for i in range(P - 10 + 64 * k)) for k in range(4)]  # ends at byte P of block k
+    runs = [(gpu_ctx, msgs[k], 2 + k) for k in range(3)] + [(gpu_ctx, msgs[3], 1)]
+    runs += [(generic_pad_ctx, msgs[k], 1) for k in range(3)]
+    for ctx, msg, pad in runs:
         want = oracle.search(msg, lo, hi, threads=8)
         for td in (0, 2):
             ctx.set_task_digits(td)
@@ -181,14 +184,15 @@ def _layout_ranges():
 def test_layout_full_range_goldens(gpu_ctx, case):
     """Round 4's kernels at full size: a whole 2^32-nonce 10-digit range for
     a padc message (L = 50, and L = 46 with the two-word inner loop), a
-    generic padding-block one after a prefix block (L = 114), and an NBV = 2
+    padding-block one after a prefix block (L = 114: search_kernel_padk<P, 1>
+    since round 5, the generic kernel before), and an NBV = 2
     one (L = 59), against the AVX-512 oracle's full scans
     (tests/golden/make_layout_golden.py); the launch stats name the kernel."""
     msg = bytes.fromhex(case["msg_hex"])
     assert gpu_ctx.search(msg, case["lower"], case["upper"]) == (case["hash"], case["nonce"])
     st = gpu_ctx.last_stats()
     dom = max((st.launch[i] for i in range(st.recorded)), key=lambda x: x.nonces)
-    want = {50: (1, 2), 46: (1, 2), 114: (1, 1), 59: (2, 0)}[case["len"]]
+    want = {50: (1, 2), 46: (1, 2), 114: (1, 3), 59: (2, 0), 178: (1, 4)}[case["len"]]  # 114, 178: padk<P, K>
     assert (dom.nbv, dom.pad_block) == want, (dom.nbv, dom.pad_block)
 
 

@@ -491,8 +491,9 @@ def test_guard_on_the_built_assembly(name):
         pytest.skip("device assembly not built (make -C distributed_bitcoin_minter_amd/csrc)")
     orig = open(src).readlines()
     st = guard.check(orig, _passes(orig), ["search_kernel"])
-    # 8 search_kernel<P, 1> per range, + search_kernel_padc<P> for P = 56..63
-    assert st["kernels"] == {"inst1_16_23": 8, "inst1_56_63": 16}[name]
+    # 8 search_kernel<P, 1> per range, + search_kernel_padc<P> and
+    # search_kernel_padk<P, 1>, <P, 2> for P = 56..63
+    assert st["kernels"] == {"inst1_16_23": 8, "inst1_56_63": 32}[name]
     assert st["inserted"] > 1000 and st["rewritten"] > 0 and st["deleted"] == 0
     guard.check(orig, _passes(orig, drop=2), ["search_kernel"])
     if name == "inst1_56_63":

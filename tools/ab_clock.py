@@ -52,7 +52,7 @@ def main():
     b = phase(prod, probe, reps)
     prod.close()
     probe.close()
-    bound = lambda ghz: bench.issue_bound(18, 1, ghz)["GHs_per_gpu"]
+    bound = lambda ghz: bench.issue_bound("18:1", ghz)["GHs_per_gpu"]
     rate = (a["prod"] + b["prod"]) / 2
     incall = (a["clock"] + b["clock"]) / 2
     out = {"prod_GHs": round(rate, 3), "probe_GHs": round((a["probe"] + b["probe"]) / 2, 3),

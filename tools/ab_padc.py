@@ -12,8 +12,9 @@ launch's rate for each and their ratio, and checks the two answers agree.
 AB_LIBS="name=path.so ..." adds one more context per library build (e.g. a
 build with another bm_prio.py option or kernel macro), alternating with the
 two above; ratios are against the generic kernel of the product library.
-AB_LENS="109-117" sweeps other message lengths (there: two-block messages,
-which every build runs with the generic padding-block kernel).
+AB_LENS="109-117" sweeps other message lengths: there the messages have one
+prefix block, which the default context runs with search_kernel_padk<P, 1>
+since round 5, and "173-181" two (search_kernel_padk<P, 2>).
 """
 import json
 import os

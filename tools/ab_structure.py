@@ -39,7 +39,7 @@ def main():
                 wall = time.perf_counter() - t
                 st = ctx.last_stats()
                 dom = max((st.launch[i] for i in range(st.recorded)), key=lambda x: x.nonces)
-                ib = bench.issue_bound(dom.p, dom.nbv, dom.clock_ghz) if dom.clock_ghz > 0 else None
+                ib = bench.issue_bound(bench.isa_key(dom.p, dom.nbv, dom.pad_block), dom.clock_ghz) if dom.clock_ghz > 0 else None
                 rate = (hi - lo + 1) / wall / 1e9
                 res[name].append({"GHs": rate, "span_GHs": (hi - lo + 1) / st.span_ms / 1e6,
                                   "clock": dom.clock_ghz, "launches": st.launches,

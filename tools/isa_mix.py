@@ -7,7 +7,8 @@ every slow op takes an issue slot of its own, fast ops fill the second slot
 beside it.  Writes distributed_bitcoin_minter_amd/csrc/
 isa_mix.json, which bench.py reads to report the issue bound.
 
-    python tools/isa_mix.py 18:1 12:1 56:c ...  (P:NBV pairs, P:c = search_kernel_padc<P>; default 18:1 12:1;
+    python tools/isa_mix.py 18:1 12:1 56:c 60:k1 ...  (P:NBV pairs, P:c = search_kernel_padc<P>,
+                                                P:kK = search_kernel_padk<P, K>; default 18:1 12:1;
                                                 "all": every layout)
 """
 import json
@@ -72,15 +73,23 @@ def asm_file(p, nbv):
 def main():
     pairs = sys.argv[1:] or ["18:1", "12:1"]
     if pairs == ["all"]:  # every layout the library instantiates (bm_inst.hip)
-        pairs = [f"{p}:1" for p in range(64)] + [f"{p}:2" for p in range(19)] + [f"{p}:c" for p in range(55, 64)]
+        pairs = ([f"{p}:1" for p in range(64)] + [f"{p}:2" for p in range(19)] + [f"{p}:c" for p in range(55, 64)]
+                 + [f"{p}:k{k}" for k in (1, 2) for p in range(55, 64)])
     out = {"cycles_per_slot": CYC_SLOT, "model": "slots per 64 nonces = max(slow, (slow + fast) / 2)",
            "source": "tools/isa_mix.py on the built assembly (hipcc -O3 gfx950 + csrc/bm_prio.py)", "layouts": {}}
     for pr in pairs:
-        # "P:c" = search_kernel_padc<P> (padding-block layout of a one-block message)
+        # "P:c" = search_kernel_padc<P> (padding-block layout of a one-block
+        # message), "P:kK" = search_kernel_padk<P, K> (the same after K prefix blocks)
         p, kind = pr.split(":")
-        p, padc = int(p), kind == "c"
-        nbv = 1 if padc else int(kind)
-        ops = inner_ops(asm_file(p, nbv), f"search_kernel_padcILi{p}ELi1E" if padc else f"search_kernelILi{p}ELi{nbv}E")
+        p = int(p)
+        if kind == "c":
+            nbv, sym = 1, f"search_kernel_padcILi{p}ELi1E"
+        elif kind.startswith("k"):
+            nbv, sym = 1, f"search_kernel_padkILi{p}ELi{int(kind[1:])}ELi1E"
+        else:
+            nbv = int(kind)
+            sym = f"search_kernelILi{p}ELi{nbv}E"
+        ops = inner_ops(asm_file(p, nbv), sym)
         fast, slow = classify(ops)
         slots = max(slow, (slow + fast) / 2)
         out["layouts"][pr] = {"valu_fast": fast, "valu_slow": slow, "valu": fast + slow,

@@ -84,7 +84,7 @@ def sweep(args):
             if dom_ghs:
                 line["canonical_frac"] = round(dom_ghs * 1e9 * c * bench.OPS_PER_COMPRESSION / 1e12 /
                                                bench.VALU_PEAK_T, 4)
-                ib = bench.issue_bound(p, "c" if pad == 2 else nbv, clock or 1.0)
+                ib = bench.issue_bound(bench.isa_key(p, nbv, pad), clock or 1.0)
                 if ib:
                     line["valu_static"] = ib["valu_per_nonce"]
                     line["executed_frac"] = round(dom_ghs * 1e9 * ib["valu_per_nonce"] / 1e12 / bench.VALU_PEAK_T, 4)
@@ -130,8 +130,8 @@ def merge(sweep_path, pass_path, csv_path):
         sys.exit(f"{len(disp)} search-kernel dispatches under PMC, {len(planned)} launches printed by the pass")
     per = collections.defaultdict(lambda: [0.0, 0])  # (P, NBV or "c") -> [VALU lane-ops, nonces]
     for d, (p, nbv, nonces, *pad) in zip(disp, planned):
-        kind = "c" if pad and pad[0] == 2 else nbv  # "c": search_kernel_padc<P>
-        name = f"search_kernel_padc<{p}, 1>" if kind == "c" else f"search_kernel<{p}, {nbv}>"
+        kind = bench.isa_key(p, nbv, pad[0] if pad else 0).split(":")[1]  # "c" padc, "kK" padk<P, K>
+        name = bench.kernel_name(p, nbv, pad[0] if pad else 0)
         if name not in names[d]:
             sys.exit(f"dispatch {d} is {names[d]}, the pass planned {name}")
         per[(p, kind)][0] += valu[d] * 64

@@ -55,8 +55,8 @@ def main():
             want = oracle.search(msg, lo, hi, threads=threads)
             st = ctx.last_stats()
             for k in range(st.recorded):
-                layouts.add((st.launch[k].nbv, st.launch[k].p, st.launch[k].pad_block == 2))
-                padc += st.launch[k].pad_block == 2
+                layouts.add((st.launch[k].nbv, st.launch[k].p, st.launch[k].pad_block >= 2))
+                padc += st.launch[k].pad_block >= 2
             nonces += hi - lo + 1
             if got != want:
                 print(json.dumps({"ok": False, "case": i, "msg_hex": msg.hex(), "lower": lo, "upper": hi,

@@ -38,7 +38,9 @@ main_nonces = {}
 lj = os.path.join(src, f"pmc_{cfg}_launches.json") if cfg else None
 if lj and os.path.exists(lj):
     for x in json.load(open(lj)):
-        name = f"search_kernel_padc<{x['p']}, 1>" if x["pad_block"] == 2 else f"search_kernel<{x['p']}, {x['nbv']}>"
+        name = (f"search_kernel_padc<{x['p']}, 1>" if x["pad_block"] == 2 else
+                f"search_kernel_padk<{x['p']}, {x['pad_block'] - 2}, 1>" if x["pad_block"] > 2 else
+                f"search_kernel<{x['p']}, {x['nbv']}>")
         main_nonces[name] = max(main_nonces.get(name, 0), x["nonces"])
 res = {}
 for k, disp in per.items():
