@@ -76,7 +76,8 @@ Also reported:
                 "system": one LSP server + N single-threaded CPU miner processes
                 + a client over the same window; "optimized": the oracle's
                 16-lane AVX-512 scan (a tuned CPU, not the reference's loop) on
-                the same cores and window.
+                the same cores and window; "go_shape": the loop with
+                hash.go's four heap allocations per nonce.
 """
 import argparse
 import glob
@@ -378,7 +379,35 @@ def cpu_baseline(target_s=3.0):
         out["optimized"] = cpu_optimized_baseline(oracle, threads, hi - n + 1, hi, want)
     except Exception as e:  # informational, like the system leg
         out["optimized"] = {"error": repr(e)}
+    try:
+        out["go_shape"] = cpu_go_shape_baseline(oracle, threads, hi - n + 1, hi, want)
+    except Exception as e:  # informational, like the system leg
+        out["go_shape"] = {"error": repr(e)}
     return out
+
+
+def cpu_go_shape_baseline(oracle, threads, lo, hi, want, target_s=1.5):
+    """The reference's loop with its per-call allocations (the
+    port above formats into one reused buffer, while hash.go:11-15 allocates
+    a digest, the Sprintf string, its []byte copy and Sum(nil)'s slice per
+    nonce): the same OpenSSL hash, each of those four objects malloc'd and
+    freed per nonce, the nonce through printf's %llu (oracle use_openssl = 2).
+    Still C, not Go: no garbage collector and no fmt reflection, so it is an
+    upper bound on what N Go miner processes reach on these cores."""
+    n = 1 << 20
+    t = time.perf_counter()
+    oracle.search(MSG_C2, hi - n + 1, hi, threads=threads, go_shape=True)
+    rate = n / (time.perf_counter() - t)
+    n = int(min(hi - lo + 1, max(n, rate * target_s)))
+    t = time.perf_counter()
+    got = oracle.search(MSG_C2, hi - n + 1, hi, threads=threads, go_shape=True)
+    dt = time.perf_counter() - t
+    ok = got == want if n == hi - lo + 1 else got == oracle.search(MSG_C2, hi - n + 1, hi, threads=threads,
+                                                                   openssl=True)
+    return {"value": n / dt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port, hash.go allocation shape",
+            "seconds": round(dt, 2), "result_ok": ok,
+            "sample": f"msg 'bradfitz', last {n} nonces of [0, 2^32-1], {threads} threads, per nonce: malloc'd "
+                      f"digest + formatted string (printf %llu) + its copy + 32-byte sum, OpenSSL SHA256, freed"}
 
 
 def cpu_optimized_baseline(oracle, threads, lo, hi, want, target_s=1.5):

@@ -14,6 +14,7 @@
 #include "bm_oracle.h"
 
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -114,6 +115,31 @@ static uint64_t hash_with(uint8_t* buf, size_t cap, const uint8_t* msg, size_t l
     uint8_t dig[32];
     size_t n = oracle_format(msg, len, nonce, buf, cap);
 #ifdef BM_ORACLE_OPENSSL
+    if (use_openssl == 2) {
+        /* hash.go:11-15 allocates per call: sha256.New() a digest, fmt.Sprintf
+         * the "%s %d" string, []byte(...) its copy, Sum(nil) the 32-byte
+         * slice.  The same four heap objects here, each malloc'd and freed per
+         * nonce, and the decimal digits through printf's %llu as Sprintf's %d */
+        (void)n;
+        SHA256_CTX* c = (SHA256_CTX*)malloc(sizeof *c);
+        char* s = (char*)malloc(cap);
+        if (len) memcpy(s, msg, len);
+        s[len] = ' ';
+        const int k = snprintf(s + len + 1, cap - len - 1, "%llu", (unsigned long long)nonce);
+        const size_t m = len + 1 + (size_t)k;
+        uint8_t* b = (uint8_t*)malloc(m);
+        memcpy(b, s, m);
+        SHA256_Init(c);
+        SHA256_Update(c, b, m);
+        uint8_t* sum = (uint8_t*)malloc(32);
+        SHA256_Final(sum, c);
+        const uint64_t h = be64(sum);
+        free(sum);
+        free(b);
+        free(s);
+        free(c);
+        return h;
+    }
     if (use_openssl) {
         /* low-level API: OpenSSL 3's one-shot SHA256() re-fetches the EVP
          * provider on every call, which is ~10x slower than the block code */

@@ -54,7 +54,12 @@ void oracle_search_excl(const uint8_t* msg, size_t len, uint64_t lower, uint64_t
  * which equals the sequential strict-'<' scan.
  * use_openssl != 0 hashes with OpenSSL's SHA256() (SHA-NI) instead of the
  * scalar restatement: same bytes, same answer, faster (used for goldens over
- * 2^32 nonces and as the CPU baseline).  Returns 0 on success. */
+ * 2^32 nonces and as the CPU baseline).  use_openssl = 2 does the same with
+ * hash.go:11-15's per-call allocation shape: a fresh heap digest
+ * (sha256.New), a fresh formatted string (fmt.Sprintf, the nonce through
+ * printf's %llu), its []byte copy, and a fresh 32-byte sum (Sum(nil)), all
+ * freed per nonce -- bench.py's cpu_baseline.go_shape leg.  Returns 0 on
+ * success. */
 int oracle_search_mt(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper,
                      int nthreads, int use_openssl,
                      uint64_t* out_hash, uint64_t* out_nonce);

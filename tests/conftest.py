@@ -69,12 +69,14 @@ class Oracle:
     def hash(self, msg: bytes, nonce: int) -> int:
         return self.lib.oracle_hash(msg, len(msg), nonce)
 
-    def search(self, msg: bytes, lo: int, hi: int, threads: int = 1, openssl: bool = False):
+    def search(self, msg: bytes, lo: int, hi: int, threads: int = 1, openssl: bool = False, go_shape: bool = False):
+        """go_shape: OpenSSL with hash.go's per-call allocations (use_openssl = 2)."""
         h, n = ctypes.c_uint64(), ctypes.c_uint64()
-        if threads == 1 and not openssl:
+        if threads == 1 and not openssl and not go_shape:
             self.lib.oracle_search(msg, len(msg), lo, hi, ctypes.byref(h), ctypes.byref(n))
         else:
-            assert self.lib.oracle_search_mt(msg, len(msg), lo, hi, threads, 1 if openssl else 0,
+            mode = 2 if go_shape else 1 if openssl else 0
+            assert self.lib.oracle_search_mt(msg, len(msg), lo, hi, threads, mode,
                                              ctypes.byref(h), ctypes.byref(n)) == 0
         return h.value, n.value
 

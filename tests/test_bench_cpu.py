@@ -329,3 +329,12 @@ def test_kernel_names_and_isa_keys():
 
 def test_rccl_version_str():
     assert bench.rccl_version_str(22703) == "2.27.3" and bench.rccl_version_str(0) is None
+
+
+def test_cpu_go_shape_baseline_small(oracle):
+    """cpu_baseline.go_shape: the reference loop with hash.go's per-call
+    allocations, on a small window; its answer equals the oracle's."""
+    lo, hi = 2 ** 32 - (1 << 21), 2 ** 32 - 1
+    want = oracle.search(b"bradfitz", lo, hi, threads=4, openssl=True)
+    got = bench.cpu_go_shape_baseline(oracle, 4, lo, hi, want, target_s=0.05)
+    assert got["result_ok"] and got["value"] > 0 and got["cores"] == 4 and "allocation" in got["kind"], got

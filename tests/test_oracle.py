@@ -57,9 +57,14 @@ def test_full_range_goldens(oracle):
 
 
 def test_openssl_and_scalar_agree(oracle):
-    msg = b"The quick brown fox"
-    for lo, hi in [(0, 5000), (U64 - 5000, U64), (999_999_000, 1_000_001_000)]:
-        assert oracle.search(msg, lo, hi, threads=4, openssl=True) == oracle.search(msg, lo, hi)
+    """The OpenSSL block code, and the same with hash.go's per-call
+    allocations (bench.py's go_shape leg; printf's %llu for the digits),
+    equal the scalar restatement, raw bytes and 20-digit nonces included."""
+    for msg in (b"The quick brown fox", bytes(range(256)) * 2, b""):
+        for lo, hi in [(0, 5000), (U64 - 5000, U64), (999_999_000, 1_000_001_000)]:
+            want = oracle.search(msg, lo, hi)
+            assert oracle.search(msg, lo, hi, threads=4, openssl=True) == want
+            assert oracle.search(msg, lo, hi, threads=3, go_shape=True) == want
 
 
 def test_x16_scanner_agrees_with_oracle(oracle):
