@@ -22,12 +22,13 @@
 #   lensweep    tools/len_sweep.py: GH/s and the three roofline fractions for every message length 0..130
 #               (every layout a 10-digit search hits); lensweep_pmc: its SQ_INSTS_VALU pass
 #   ab_padc     A/B of search_kernel_padc against the generic padding-block kernel (L = 45..53)
+#   ab_padk     the same for search_kernel_padk<P, 1> (L = 109..117) and <P, 2> (L = 173..181)
 #   parity_pad  the padding-block parity tests and every kernel layout
 #   ab          A/B of library variants: AB_LIBS="a.so b.so" (parity of each first, then alternating)
-# Logs and profiles land in gpurun_out/$TAG (TAG defaults to r04).
+# Logs and profiles land in gpurun_out/$TAG (TAG defaults to r05).
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 step() {  # name, seconds, command...
@@ -97,6 +98,9 @@ for phase in "$@"; do
       step len_sweep_pmcpass 300 env BTCMINER_STREAMS=1 BTCMINER_TAIL=0 rocprofv3 --pmc SQ_INSTS_VALU \
         -d "$OUT/pmc_lensweep" -o p --output-format csv -- python3 tools/len_sweep.py --pmc-pass --max-len 130 ;;
     ab_padc) step ab_padc 600 python -u tools/ab_padc.py ${AB_REPS:-5} ;;
+    ab_padk)
+      step ab_padk1 300 env AB_LENS=109-117 python -u tools/ab_padc.py ${AB_REPS:-5}
+      step ab_padk2 300 env AB_LENS=173-181 python -u tools/ab_padc.py ${AB_REPS:-5} ;;
     structure)
       # C2's 11 launches against one 10-digit range of the same size, live clock
       step structure 300 python -u tools/ab_structure.py 8

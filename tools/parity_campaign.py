@@ -6,8 +6,9 @@
 Each case: a random raw-byte message (0..700 bytes, any byte value), a random
 digit class 1..20, a random window of 1..2^22 nonces inside it (clipped at
 2^64-1), and sometimes a window that straddles a power of ten.  Task size and
-planner window cap are randomized too.  Kernels are counted per layout,
-search_kernel_padc apart from search_kernel.  bm_search_gpu must equal the CPU
+planner window cap are randomized too.  Kernels are counted per layout, the
+folded padding-block kernels (search_kernel_padc, search_kernel_padk<P, K>:
+stats pad_block = 2 + K) apart from search_kernel.  bm_search_gpu must equal the CPU
 oracle's sequential scan (hash.go:11-15 + miner.go:59-65, inclusive bounds)
 bit for bit.  Prints one JSON summary line; exits 1 on the first mismatch.
 The oracle is the checker only (test infrastructure)."""
@@ -35,7 +36,7 @@ def main():
     nonces = 0
     t0 = time.perf_counter()
     layouts = set()
-    padc = 0  # launches of search_kernel_padc (a one-block message's padding-block layouts)
+    folded = {}  # pad_block (2 + K) -> launches of the folded padding-block kernels
     with Context(devices=[0]) as ctx:
         for i in range(cases):
             L = rng.choice([rng.randint(0, 130), rng.randint(0, 700)])
@@ -55,8 +56,10 @@ def main():
             want = oracle.search(msg, lo, hi, threads=threads)
             st = ctx.last_stats()
             for k in range(st.recorded):
-                layouts.add((st.launch[k].nbv, st.launch[k].p, st.launch[k].pad_block >= 2))
-                padc += st.launch[k].pad_block >= 2
+                pb = st.launch[k].pad_block
+                layouts.add((st.launch[k].nbv, st.launch[k].p, pb if pb >= 2 else 0))
+                if pb >= 2:
+                    folded[pb] = folded.get(pb, 0) + 1
             nonces += hi - lo + 1
             if got != want:
                 print(json.dumps({"ok": False, "case": i, "msg_hex": msg.hex(), "lower": lo, "upper": hi,
@@ -65,7 +68,9 @@ def main():
             if (i + 1) % 200 == 0:
                 print(f"{i + 1} cases ok, {nonces} nonces, {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     print(json.dumps({"ok": True, "cases": cases, "seed": seed, "nonces": nonces, "layouts_hit": len(layouts),
-                      "padc_layouts_hit": sum(1 for x in layouts if x[2]), "padc_launches": padc,
+                      "padc_layouts_hit": sum(1 for x in layouts if x[2] == 2),
+                      "padk_layouts_hit": {f"K={pb - 2}": sum(1 for x in layouts if x[2] == pb) for pb in (3, 4)},
+                      "folded_launches": {f"K={pb - 2}": n for pb, n in sorted(folded.items())},
                       "seconds": round(time.perf_counter() - t0, 1), "oracle_threads": threads}), flush=True)
     return 0
 
