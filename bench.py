@@ -583,6 +583,7 @@ def step_record(st):
     against the earliest device's."""
     nd = st.devices
     return {"nonces": st.nonces, "span_ms": st.span_ms, "combine": COMBINED_NAMES.get(st.combine_used, "?"),
+            "launches": getattr(st, "launches", 0),
             "rccl_status": st.rccl_status, "rccl_nranks": st.rccl_nranks, "rccl_rank": st.rccl_rank,
             "devices": [(st.dev_nonces[i], st.dev_span_ms[i]) for i in range(nd)],
             "dev_rccl": [(st.dev_rccl_rank[i], st.dev_rccl_device[i]) for i in range(nd)],
@@ -1075,7 +1076,9 @@ def main():
         roof["executed"] = executed_roofline(dom.nonces, dom_ms, (pm or {}).get("valu_per_nonce"), pmc_src,
                                              static and static["valu_per_nonce"], ib_clock)
         if calls:
-            roof["call"] = call_roofline(calls, ctx.last_stats().launches, pers[-1]["nonces"],
+            # the timed steps' own launch count (the context's last call may be
+            # the C4 step by now)
+            roof["call"] = call_roofline(calls, pers[-1]["launches"], pers[-1]["nonces"],
                                          ib if world == 1 and n == 1 else None)
         out["roofline"] = roof
     if world > 1 and any(c is not None for c in clocks):

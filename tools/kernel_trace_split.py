@@ -30,13 +30,24 @@ for name, per in ids.items():
     by[name] = per[order[0]]
     if len(order) > 1:
         out_ids[name] = {k: {"calls": len(v), "max_ms": round(max(v), 3)} for k, v in per.items()}
+# Main launches: the cluster around the median of the longer half of a
+# template's launches (the timed steps' main pieces); shorter ones are the
+# tail pieces and other calls' small launches; much longer ones (>= 2x) are
+# other calls' big launches -- since round 5 every bench line ends with a C4
+# step, whose 10-digit launch of the same template runs 9e9 nonces while its
+# other stream's launches stretch it, and which must not count as a main one.
 out = {}
 for name, ds in sorted(by.items(), key=lambda kv: -max(kv[1])):
-    top = max(ds)
-    main = [d for d in ds if d > 0.5 * top]
-    rest = [d for d in ds if d <= 0.5 * top]
+    top_half = sorted(ds)[len(ds) // 2:]
+    ref = top_half[len(top_half) // 2]
+    main = [d for d in ds if 0.5 * ref < d < 2 * ref]
+    rest = [d for d in ds if d <= 0.5 * ref]
+    big = [d for d in ds if d >= 2 * ref]
     out[name] = {"calls": len(ds), "main_calls": len(main), "main_avg_ms": round(sum(main) / len(main), 3),
                  "other_calls": len(rest), "other_avg_ms": round(sum(rest) / len(rest), 3) if rest else None}
+    if big:
+        out[name]["long_calls"] = len(big)
+        out[name]["long_ms"] = [round(d, 3) for d in big]
 if out_ids:
     out["_kernel_ids"] = {"note": "templates dispatched from more than one code object; the entries above use "
                                   "the first (the product library)", "ids": out_ids}
