@@ -338,3 +338,35 @@ def test_cpu_go_shape_baseline_small(oracle):
     want = oracle.search(b"bradfitz", lo, hi, threads=4, openssl=True)
     got = bench.cpu_go_shape_baseline(oracle, 4, lo, hi, want, target_s=0.05)
     assert got["result_ok"] and got["value"] > 0 and got["cores"] == 4 and "allocation" in got["kind"], got
+
+
+def test_c4_block_one_process_and_ranks():
+    """bench.c4_block on CPU with a stand-in context: one C4 step over
+    [0, 2^40-1] (strong scaling), checked against the committed 2^40 golden,
+    per device (one process) or per rank (over a real 2-rank rendezvous in
+    test_bench_ranks_join_together's harness; here world 1) with nonces,
+    span, rate, start offset and allgather time."""
+    from types import SimpleNamespace as NS
+    want = bench.golden(b"bradfitz", 0, 2 ** 40 - 1)
+
+    class Ctx:
+        def search(self, msg, lo, hi):
+            assert (msg, lo, hi) == (b"bradfitz", 0, 2 ** 40 - 1)
+            return tuple(want)
+
+        def last_stats(self):
+            half = 2 ** 39
+            return NS(nonces=2 ** 40, span_ms=20000.0, combine_used=2, rccl_status=0, rccl_nranks=0, rccl_rank=-1,
+                      devices=2, dev_nonces=[half, half], dev_span_ms=[19990.0, 20000.0], dev_rccl_rank=[-1, -1],
+                      dev_rccl_device=[-1, -1], rccl_version=22703, rccl_init_ms=0.0, rccl_allgather_ms=0.0,
+                      combine_ms=0.02, start_threads=2, dev_start_ms=[0.0, 0.05], dev_allgather_ms=[0.0, 0.0],
+                      launches=14)
+
+    ctx = Ctx()
+    c4 = bench.c4_block(NS(), ctx, bench.Group(), ctx.search, 2)
+    assert (c4["lower"], c4["upper"], c4["nonces"], c4["scaling"]) == (0, 2 ** 40 - 1, 2 ** 40, "strong")
+    assert c4["result_ok"] is True and c4["result"] == want and c4["combine"] == "host"
+    assert [d["nonces"] for d in c4["devices"]] == [2 ** 39, 2 ** 39] and c4["devices"][1]["start_ms"] == 0.05
+    assert c4["GHs"] > 0 and c4["seconds"] >= 0
+    # the step record keeps the timed call's launch count (the line's call roofline uses it)
+    assert bench.step_record(ctx.last_stats())["launches"] == 14
