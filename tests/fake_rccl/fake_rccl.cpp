@@ -140,8 +140,12 @@ ncclResult_t ncclCommInitRankConfig(ncclComm_t* out, int nranks, ncclUniqueId id
     c->sh = static_cast<Shared*>(m);  // a fresh file is zeros: no posts, nobody joined
     if (hipGetDevice(&c->dev) != hipSuccess ||
         hipHostMalloc(&c->h_send, kMaxBytes, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&c->h_recv, kMaxBytes * kMaxRanks, hipHostMallocDefault) != hipSuccess)
+        hipHostMalloc(&c->h_recv, kMaxBytes * kMaxRanks, hipHostMallocDefault) != hipSuccess) {
+        if (c->h_send) (void)hipHostFree(c->h_send);
+        munmap(m, sizeof(Shared));
+        delete c;
         return ncclUnhandledCudaError;
+    }
     c->sh->joined.fetch_add(1);
     while (c->sh->joined.load() < nranks) std::this_thread::sleep_for(std::chrono::milliseconds(1));
     if (rank == 0) unlink(path.c_str());  // every rank has it mapped by now
