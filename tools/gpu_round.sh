@@ -14,6 +14,7 @@
 #   bench       C2 bench line, 20 steps (the driver's N = 1 line); bench_c3, bench_c4: C3 / C4 on one GPU
 #   rehearse    the multi-GPU modes on one GPU: one process 2-way split, 2 torchrun ranks under a
 #               per-rank visibility mask, C4 over 8 one-process slots; rehearse8: 8 torchrun ranks on GPU 0
+#   rehearse_fake  2 and 8 torchrun ranks on GPU 0 with the group joined through the stand-in RCCL
 #   c5          C5 at size: the native (C++) system and the Python one
 #   prof        rocprofv3 kernel traces of C2 (2 streams, 1 stream) and C3
 #   prof_driver rocprofv3 kernel trace of the driver's exact bench command
@@ -66,6 +67,16 @@ for phase in "$@"; do
       # the driver's N = 8 launch, all 8 ranks masked onto GPU 0 (RCCL refuses: rendezvous gather)
       step rehearse8_torchrun 400 env HIP_VISIBLE_DEVICES=0 python -u -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 --steps 2 --warmup 2 ;;
+    rehearse_fake)
+      # the driver's N = 2 / N = 8 launch shapes with the group JOINED: the
+      # library linked against the stand-in RCCL (tests/fake_rccl/), every rank
+      # on GPU 0 -- the joined-group path real RCCL refuses on one GPU
+      step rehearse2_fakerccl 400 env HIP_VISIBLE_DEVICES=0 BTCMINER_LIB=$PWD/tests/fake_rccl/libbtcminer_fakerccl.so \
+        python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 \
+        bench.py --gpus 2 --steps 3 --warmup 2
+      step rehearse8_fakerccl 400 env HIP_VISIBLE_DEVICES=0 BTCMINER_LIB=$PWD/tests/fake_rccl/libbtcminer_fakerccl.so \
+        python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29520 \
+        bench.py --gpus 8 --steps 2 --warmup 2 ;;
     c5)
       step c5_native 300 python -u tools/bench_c5_native.py
       step c5_python 300 python -u tools/bench_c5.py ;;
