@@ -672,7 +672,8 @@ def rccl_costs(slots, version):
                      "combine_ms_max": round(max(s.get("combine_ms", 0.0) for s in slots), 4),
                      "per_step": "allgather_ms: HIP events around each slot's allgather on its stream, from the end "
                                  "of its own work (so the wait for the slowest slot is inside); combine_ms: the "
-                                 "library's host time for the whole combine stage"}}
+                                 "library's host time from the end of the slot's own work to the end of its "
+                                 "combine (the same wait, the allgather, the result copy)"}}
 
 
 def c4_block(args, ctx, grp, search, n):

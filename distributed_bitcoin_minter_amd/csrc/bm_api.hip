@@ -693,10 +693,19 @@ int combine_local(bm_ctx* ctx, Partial* best_out) {
                                   d.stream));
         }
     }
+    // the end of every device's own work (its reduction, bal[1]) seen on the
+    // host: from there on the wait is the combine's (bm_stats_t.combine_ms)
+    if (ctx->balance || ctx->timing)
+        for (int di = 0; di < ndev; ++di) {
+            BM_HIP(hipSetDevice(ctx->devs[di].id));
+            BM_HIP(hipEventSynchronize(ctx->devs[di].bal[1]));
+        }
+    const auto t_own = std::chrono::steady_clock::now();
     for (int di = 0; di < ndev; ++di) {
         BM_HIP(hipSetDevice(ctx->devs[di].id));
         BM_HIP(hipStreamSynchronize(ctx->devs[di].stream));
     }
+    st.combine_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_own).count();
     st.combine_used = ctx->rank_ctx ? BM_COMBINED_LOCAL : via_rccl ? BM_COMBINED_RCCL : BM_COMBINED_HOST;
     st.rccl_status = ctx->rccl_status;
     record_rccl(ctx, via_rccl);
@@ -730,6 +739,7 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
     // the end of this rank's own work, from which the peer timeout counts
     // (without the event: from the moment the allgather is enqueued)
     const bool own_mark = posted && hipEventRecord(d.own_done, d.stream) == hipSuccess;
+    auto t_own = std::chrono::steady_clock::now();
     const bool limited = ctx->peer_timeout_ms > 0;
     int rc = BM_OK;
     bool copied = false;
@@ -754,7 +764,8 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
                                                hipMemcpyDeviceToHost, d.stream) == hipSuccess;
         // only the wait for the other ranks is bounded
         if (own_mark) (void)hipEventSynchronize(d.own_done);
-        const auto deadline = std::chrono::steady_clock::now() + timeout;
+        t_own = std::chrono::steady_clock::now();  // this rank's own work is done: the rest is the group's
+        const auto deadline = t_own + timeout;
         if (rc == BM_OK && !limited && hipStreamSynchronize(d.stream) != hipSuccess) rc = BM_EHIP;
         for (auto pause = std::chrono::microseconds(10); rc == BM_OK && limited;) {
             const hipError_t q = hipStreamQuery(d.stream);
@@ -784,6 +795,7 @@ int combine_group(bm_ctx* ctx, int own_rc, Partial* best_out) {
         return own_rc != BM_OK ? own_rc : rc;  // this rank's own failure stays the one it reports
     }
     st.combine_used = BM_COMBINED_RCCL;
+    st.combine_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_own).count();
     record_rccl(ctx, true);
     if (ctx->timing) record_allgather(ctx);
     if (!copied) return own_rc != BM_OK ? own_rc : BM_EHIP;
@@ -905,7 +917,6 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
 
     // 3. combine (a rank of a group takes part even after a failure)
     Partial best{UINT64_MAX, UINT64_MAX};
-    const auto t_combine = std::chrono::steady_clock::now();
     if (group) {
         const int grc = combine_group(ctx, rc, &best);
         if (grc != BM_OK) {
@@ -927,7 +938,6 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
             return rc;
         }
     }
-    st.combine_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_combine).count();
 
     // each device's start against the earliest device's (host submission times)
     std::vector<double> start_ms(ndev, 0.0);

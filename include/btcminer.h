@@ -231,8 +231,11 @@ typedef struct bm_stats {
                                   (first) device's stream (timing on): it starts when this
                                   device's own work is done, so it includes the wait for the
                                   slowest peer; max over the devices of a context; 0 otherwise */
-    double combine_ms;         /* host wall time of the call's combine stage (allgather or host
-                                  copies, and the final stream synchronisations) */
+    double combine_ms;         /* host time from the end of this process's own work (its devices'
+                                  reductions, seen on the host) to the end of the combine: the wait
+                                  for the peers, the allgather or host copies, the result copy.
+                                  Without timing or balance in a one-process context, from the
+                                  enqueue of the combine instead */
     double dev_allgather_ms[BM_MAX_STAT_DEVICES]; /* each device's allgather event pair (timing on) */
     double dev_start_ms[BM_MAX_STAT_DEVICES];     /* host time at which each device's first
                                   operation of the call was submitted, relative to the earliest
