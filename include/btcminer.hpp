@@ -75,6 +75,17 @@ class Context {
         check(bm_ctx_join_rank(ctx_, id, timeout_ms), "bm_ctx_join_rank");
     }
     void leave() { check(bm_ctx_leave_rank(ctx_), "bm_ctx_leave_rank"); }
+    // a joined rank's wait for its peers, at most (default BM_DEFAULT_PEER_TIMEOUT_MS; 0: no limit)
+    void set_peer_timeout(int timeout_ms) {
+        check(bm_ctx_set_peer_timeout(ctx_, timeout_ms), "bm_ctx_set_peer_timeout");
+    }
+    // per-launch HIP event timing, and what the last search reported (bm_stats_t)
+    void set_timing(bool on) { check(bm_ctx_set_timing(ctx_, on ? 1 : 0), "bm_ctx_set_timing"); }
+    bm_stats_t last_stats() const {
+        bm_stats_t s;
+        check(bm_ctx_last_stats(ctx_, &s), "bm_ctx_last_stats");
+        return s;
+    }
     Context(Context&& o) noexcept : ctx_(std::exchange(o.ctx_, nullptr)) {}
     Context& operator=(Context&& o) noexcept {
         if (this != &o) {
