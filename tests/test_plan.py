@@ -154,17 +154,19 @@ if given is not None:
         check_plan(msg, lo, hi, random.Random(len(msg) ^ lo), samples=2)
 
 
-def _padc_kw_table():
-    """pad_kw_const(P) for P = 55..63 from bm_sha256.hpp (the constants
-    search_kernel_padc folds), printed by a tiny C++ program."""
+def _padc_kw_table(K=0):
+    """pad_kw_const(P, K) for P = 55..63 from bm_sha256.hpp (the constants
+    search_kernel_padc (K = 0) and search_kernel_padk<P, K> fold), printed by
+    a tiny C++ program."""
     import os
     import subprocess
     import tempfile
     from conftest import ROOT
     src = ('#include <cstdio>\n#include "bm_sha256.hpp"\nint main() {\n'
-           '  for (int p = 55; p < 64; ++p) { const bm::KW64 k = bm::pad_kw_const(p);\n'
+           f'  for (int p = 55; p < 64; ++p) {{ const bm::KW64 k = bm::pad_kw_const(p, {K});\n'
            '    for (int t = 0; t < 64; ++t) std::printf("%u ", k.v[t]); std::printf("\\n"); }\n'
-           '  static_assert(bm::kPadKW<60>.v[15] == bm::kK256[15] + 8u * 61u, "compile-time table");\n}\n')
+           '  static_assert(bm::kPadKW<60>.v[15] == bm::kK256[15] + 8u * 61u, "compile-time table");\n'
+           '  static_assert(bm::kPadKW<60, 2>.v[15] == bm::kK256[15] + 8u * (128u + 61u), "K = 2");\n}\n')
     with tempfile.TemporaryDirectory() as d:
         c, exe = os.path.join(d, "kw.cpp"), os.path.join(d, "kw")
         open(c, "w").write(src)
@@ -174,26 +176,32 @@ def _padc_kw_table():
     return {55 + i: [int(x) for x in ln.split()] for i, ln in enumerate(out)}
 
 
-def test_padc_constants_are_the_padding_block_of_a_one_block_message():
-    """search_kernel_padc folds K[t] + W[t] of the padding block of a message
-    whose last byte sits at P >= 55 of block 0 (bm_sha256.hpp pad_kw_const).
-    Here those 64 words are rebuilt from standard SHA-256 padding (FIPS 180-4:
-    0x80, zeros, the 64-bit bit length) and the block schedule, and the full
-    two-compression hash from the IV with them equals hashlib's."""
+@pytest.mark.parametrize("Kp", [0, 1, 2])
+def test_padc_constants_are_the_padding_block_of_a_one_block_message(Kp):
+    """search_kernel_padc (Kp = 0 prefix blocks) and search_kernel_padk<P, Kp>
+    fold K[t] + W[t] of the padding block of a message whose last byte sits
+    at P >= 55 of block Kp (bm_sha256.hpp pad_kw_const(P, Kp)).  Here those 64
+    words are rebuilt from standard SHA-256 padding (FIPS 180-4: 0x80, zeros,
+    the 64-bit bit length) and the block schedule, and the full hash (the
+    message blocks from the IV, then the padding block with them) equals
+    hashlib's."""
     from sharef import K
     rot = lambda x, n: ((x >> n) | (x << (32 - n))) & 0xFFFFFFFF
-    table = _padc_kw_table()
+    table = _padc_kw_table(Kp)
     for P in range(55, 64):
-        msg = bytes(0x41 + i % 26 for i in range(P + 1))          # last byte at P of block 0
+        msg = bytes(0x41 + i % 26 for i in range(64 * Kp + P + 1))   # last byte at P of block Kp
         padded = msg + b"\x80" + b"\0" * ((55 - len(msg)) % 64) + (8 * len(msg)).to_bytes(8, "big")
-        assert len(padded) == 128
-        w = [int.from_bytes(padded[64 + 4 * i: 68 + 4 * i], "big") for i in range(16)]
-        assert w[1:15] == [0] * 14 and w[0] == (0x80000000 if P == 63 else 0) and w[15] == 8 * (P + 1)
+        assert len(padded) == 64 * (Kp + 2)
+        last = 64 * (Kp + 1)
+        w = [int.from_bytes(padded[last + 4 * i: last + 4 + 4 * i], "big") for i in range(16)]
+        assert w[1:15] == [0] * 14 and w[0] == (0x80000000 if P == 63 else 0) and w[15] == 8 * (64 * Kp + P + 1)
         for t in range(16, 64):
             s0 = rot(w[t - 15], 7) ^ rot(w[t - 15], 18) ^ (w[t - 15] >> 3)
             s1 = rot(w[t - 2], 17) ^ rot(w[t - 2], 19) ^ (w[t - 2] >> 10)
             w.append((w[t - 16] + s0 + w[t - 7] + s1) & 0xFFFFFFFF)
         assert table[P] == [(K[t] + w[t]) & 0xFFFFFFFF for t in range(64)], P
-        st = compress(compress(list(IV), [int.from_bytes(padded[4 * i: 4 * i + 4], "big") for i in range(16)]),
-                      w[:16])
+        st = list(IV)
+        for b in range(Kp + 1):
+            st = compress(st, [int.from_bytes(padded[64 * b + 4 * i: 64 * b + 4 * i + 4], "big") for i in range(16)])
+        st = compress(st, w[:16])
         assert b"".join(x.to_bytes(4, "big") for x in st) == hashlib.sha256(msg).digest()
