@@ -201,3 +201,68 @@ def test_bench_torchrun_joined_group_line():
     c4 = line["c4"]
     assert c4["result_ok"] is True and c4["combine"] == "rccl" and c4["nonces"] == 2 ** 40, c4
     assert sum(r["nonces"] for r in c4["ranks"]) == 2 ** 40 and all(r["allgather_ms"] > 0 for r in c4["ranks"])
+
+
+_RANK_DIES = r"""
+import json, os, sys, time
+sys.path.insert(0, sys.argv[1])
+from distributed_bitcoin_minter_amd import _lib
+_lib.load()
+from distributed_bitcoin_minter_amd import BtcMinerError, Context, rccl_unique_id
+from distributed_bitcoin_minter_amd.rendezvous import Rendezvous
+rz = Rendezvous(timeout_s=120)
+uid = rz.broadcast_bytes(rccl_unique_id() if rz.rank == 0 else None)
+c = Context(devices=[0], rank=rz.rank, world=rz.world)
+c.join(uid, timeout_ms=60_000)
+first = list(c.search(b"bradfitz", 0, 9999))
+rz.barrier()
+if rz.rank == 1:
+    os._exit(3)                      # dies inside the group: no leave, no close
+c.set_peer_timeout(2000)
+t = time.time()
+try:
+    c.search(b"bradfitz", 0, 9999)
+    status = 0
+except BtcMinerError as e:
+    status = e.status
+waited = time.time() - t
+t = time.time()
+c.close()                            # teardown must not wait on the dead peer
+print(json.dumps({"first": first, "status": status, "waited": round(waited, 3),
+                  "close_s": round(time.time() - t, 3)}), flush=True)
+os._exit(0)                          # no rendezvous goodbye: the peer is gone
+"""
+
+
+def test_fake_group_peer_dies():
+    """A rank of a joined group dies (exits without leaving) after a search:
+    the survivor's next search returns BM_ETIMEDOUT after its peer timeout
+    instead of waiting for ever, and closing its context returns promptly
+    (the communicator is aborted, never waited on)."""
+    _need_fake()
+    from distributed_bitcoin_minter_amd._lib import BM_ETIMEDOUT
+    import shutil
+    import tempfile
+    before = set(glob.glob("/dev/shm/fakerccl-*"))
+    port = _port()
+    rdzv = tempfile.mkdtemp(prefix="btcminer-rdzv-dies-")  # the ranks exit without the rendezvous goodbye
+    procs = []
+    try:
+        for r in range(2):
+            env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                       WORLD_SIZE="2", BTCMINER_LIB=FAKE_LIB, BTCMINER_RDZV_DIR=rdzv)
+            procs.append(subprocess.Popen([sys.executable, "-c", _RANK_DIES, ROOT], env=env, stdout=subprocess.PIPE,
+                                          stderr=subprocess.PIPE, text=True))
+        outs = [p.communicate(timeout=180) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        _cleanup_shm(before)
+        shutil.rmtree(rdzv, ignore_errors=True)
+    assert procs[1].returncode == 3, outs[1][1][-2000:]
+    assert procs[0].returncode == 0, outs[0][1][-3000:]
+    o = json.loads(outs[0][0].strip().splitlines()[-1])
+    assert o["first"] == [1419516646206828, 9898] and o["status"] == BM_ETIMEDOUT, o
+    assert 1.5 < o["waited"] < 30 and o["close_s"] < 10, o

@@ -140,7 +140,7 @@ def merge(sweep_path, pass_path, csv_path):
         if not ln.startswith("{"):
             continue
         line = json.loads(ln)
-        v = per.get((line["P"], "c" if line.get("pad") == 2 else line["nbv"]))
+        v = per.get((line["P"], bench.isa_key(line["P"], line["nbv"], line.get("pad") or 0).split(":")[1]))
         if v and v[1] and line.get("dom_GHs"):
             line["valu_pmc"] = round(v[0] / v[1], 1)
             line["executed_frac_pmc"] = round(line["dom_GHs"] * 1e9 * line["valu_pmc"] / 1e12 / bench.VALU_PEAK_T, 4)
