@@ -306,6 +306,8 @@ def test_one_process_device_summaries(monkeypatch):
     assert [s["rccl_rank"] for s in slots] == [0, 1, 2, 3] and [s["rccl_device"] for s in slots] == [0, 1, 2, 3]
     assert len({s["pci_bus_id"] for s in slots}) == 4 and all(s["combine"] == "rccl" for s in slots)
     assert bench.scaling_validity(4, slots, "rccl", False) == {"scaling_valid": True}
+    # ABI 7 figures absent from this stand-in: zeros, and the RCCL block still forms
+    assert [s["start_ms"] for s in slots] == [0.0] * 4 and bench.rccl_costs(slots, 0)["rccl"]["version_str"] is None
     slots = bench.device_summaries([bench.step_record(stats(_lib.BM_COMBINED_HOST, 0))], [0, 1, 2, 3])
     v = bench.scaling_validity(4, slots, "rccl", False)
     assert v["scaling_valid"] is False and "combine host" in v["scaling_invalid"][0]
