@@ -326,6 +326,8 @@ def test_kernel_names_and_isa_keys():
     for p in range(55, 64):
         for k in (1, 2):
             assert lay[f"{p}:k{k}"]["issue_slots"] <= lay[f"{p}:1"]["issue_slots"], (p, k)
+            assert lay[f"{p}:k{k}"]["readlanes"] == 0, (p, k)  # no spilled SGPR read back per nonce
+    assert lay["56:1"]["readlanes"] == 24  # the generic kernel's (messages with >= 3 prefix blocks)
     assert bench.issue_bound("60:k1", 2.4)["GHs_per_gpu"] > bench.issue_bound("60:1", 2.4)["GHs_per_gpu"]
 
 

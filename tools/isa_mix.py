@@ -92,8 +92,13 @@ def main():
         ops = inner_ops(asm_file(p, nbv), sym)
         fast, slow = classify(ops)
         slots = max(slow, (slow + fast) / 2)
+        # v_readlane in the loop: SGPRs the compiler spilled to VGPR lanes and
+        # reads back per nonce (the generic padding-block kernel's 64 kernarg
+        # K+W words)
+        readlanes = sum(1 for op, _ in ops if op.startswith("v_readlane"))
         out["layouts"][pr] = {"valu_fast": fast, "valu_slow": slow, "valu": fast + slow,
-                                        "issue_slots": slots, "simd_cycles_per_64_nonces": slots * CYC_SLOT}
+                              "issue_slots": slots, "simd_cycles_per_64_nonces": slots * CYC_SLOT,
+                              "readlanes": readlanes}
         print(pr, out["layouts"][pr])
     json.dump(out, open(os.path.join(CSRC, "isa_mix.json"), "w"), indent=1)
 
