@@ -202,6 +202,11 @@ def test_miner_patch_applies_to_the_reference():
     imports = got.split("import (")[1].split(")")[0]
     assert '"log"' in imports and '"errors"' not in imports and "lspnet" not in imports  # :92, :5, :8
     assert "_, write_msg_err :=" not in got  # lsp.Client.Write returns one value
+    # zero Params make time.NewTicker(0) panic (lsp/client_impl.go:141)
+    assert "lsp.Params{}" not in got and "params := lsp.NewParams()" in got           # :29
+    params_go = "/root/reference/project2/lsp/params.go"
+    if os.path.exists(params_go):
+        assert "func NewParams() *Params" in open(params_go).read()
 
 
 def test_peer_timeout_default_is_bounded():
