@@ -89,10 +89,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from distributed_bitcoin_minter_amd import _lib  # noqa: E402
+from distributed_bitcoin_minter_amd import _lib, codeobj  # noqa: E402
 from distributed_bitcoin_minter_amd._lib import (COMBINED_NAMES, Context, device_count,  # noqa: E402
                                                  device_pci_bus_id, rccl_unique_id)
-from distributed_bitcoin_minter_amd.dist import lex_min, shares_from_rates  # noqa: E402
+from distributed_bitcoin_minter_amd.dist import calibrated_rates, lex_min, shares_from_rates  # noqa: E402
 
 U64 = (1 << 64) - 1
 PER_GPU = 1 << 32
@@ -513,15 +513,17 @@ class Group:
             self.rdzv.close()
 
 
-def calibrate_split(args, ctx, grp):
-    """After the warmup (ranks: at least 2 steps, so the one timed is warm):
-    each GPU's rate in the last warmup step (its own
-    nonces over its launches' span, HIP events, so the wait for the other
-    ranks does not count) -> integer shares, the same on every rank -> the
-    timed steps cut the range in proportion (bm_ctx_set_split on every rank's
-    context, joined to the RCCL group or not).  A one-process
-    multi-device context balances itself (bm_ctx_set_balance).  Returns what
-    the bench line reports."""
+def calibrate_split(args, ctx, grp, warm):
+    """After the warmup (ranks: at least 2 steps, so at least one is warm):
+    each GPU's rate in every warmup step after the first (its own nonces over
+    its launches' span, HIP events, so the wait for the other ranks does not
+    count; warm: step_record()s), made robust to a transient step
+    (dist.calibrated_rates: the median over the steps, a rank held at 0.85 of
+    the fastest unless two of its steps agree it is slower) -> integer shares,
+    the same on every rank -> the timed steps cut the range in proportion
+    (bm_ctx_set_split on every rank's context, joined to the RCCL group or not;
+    DESIGN.md §6).  A one-process multi-device context balances itself
+    (bm_ctx_set_balance).  Returns what the bench line reports."""
     if args.no_balance or args.warmup < 1:
         return {"mode": "near-equal"}
     if grp.world > 1 and args.warmup < 2:
@@ -533,15 +535,17 @@ def calibrate_split(args, ctx, grp):
             return {"mode": "one device"}
         sh = ctx.get_split()
         return {"mode": "measured device rates (bm_ctx_set_balance)", "shares": sh} if sh else {"mode": "near-equal"}
-    st = ctx.last_stats()
-    rate = st.nonces / st.span_ms if st.span_ms > 0 and st.nonces >= (1 << 30) else 0.0
-    rates = grp.gather(rate)
-    if min(rates) <= 0:
+    mine = [r["nonces"] / r["span_ms"] if r["span_ms"] > 0 and r["nonces"] >= (1 << 30) else 0.0 for r in warm[1:]]
+    steps = grp.gather(mine)
+    if min(min(r) for r in steps) <= 0:
         return {"mode": "near-equal", "note": "a rank's piece was too small to time"}
+    rates, info = calibrated_rates(steps)
     shares = shares_from_rates(rates)
     ctx.set_split(shares)
-    return {"mode": "measured rank rates, last warmup step", "shares": shares,
-            "rates_nonces_per_ms": [round(r, 1) for r in rates]}
+    return {"mode": f"measured rank rates, median of warmup steps 2..{len(warm)}", "shares": shares,
+            "rates_nonces_per_ms": [round(r, 1) for r in rates],
+            "step_rates_nonces_per_ms": [[round(x, 1) for x in r] for r in steps],
+            "spread": info["spread"], "clamped_to_0.85": info["clamped"]}
 
 
 def call_roofline(calls, launches, call_nonces, ib=None):
@@ -676,16 +680,33 @@ def rccl_costs(slots, version):
                                  "combine (the same wait, the allgather, the result copy)"}}
 
 
+def warm_layouts(search, msg, lo, hi, per=4096):
+    """One tiny untimed search at the start of every digit count of [lo, hi]:
+    each layout the range reaches has had its first launch (its code object
+    loaded) before a timed step, whatever config the line's own steps ran
+    (a C3 line's steps never launch C4's layouts).  Collective
+    under a rank group: every rank makes the same calls."""
+    calls = 0
+    for d in range(len(str(lo)), len(str(hi)) + 1):
+        a = max(lo, 10 ** (d - 1) if d > 1 else 0)
+        if a > hi:
+            break
+        search(msg, a, min(hi, a + per - 1))
+        calls += 1
+    return calls
+
+
 def c4_block(args, ctx, grp, search, n):
     """north_star's target is stated on a 2^40-nonce search, so
     every line carries one C4 step ([0, 2^40-1], 'bradfitz', strong scaling:
     the N GPUs split it) after the headline's timed region, through the same
-    context or group and the same split shares.  Warm: its layouts (P = 9..21,
-    1- to 13-digit nonces) live in the code objects the headline's steps
-    already loaded on every GPU.  Timed like the headline (barrier, one
-    search, barrier, max over ranks), checked against the committed golden
-    (the 2^40 CPU scan).  About 20 s on one GPU, 2.5 s on eight."""
+    context or group and the same split shares.  Warm: one tiny untimed
+    search per digit count first (warm_layouts: P = 9..21, 1- to 13-digit
+    nonces).  Timed like the headline (barrier, one search, barrier, max over
+    ranks), checked against the committed golden (the 2^40 CPU scan).  About
+    20 s on one GPU, 2.5 s on eight."""
     msg, lo, hi, scaling, desc = workload("C4", n)
+    warm = warm_layouts(search, msg, lo, hi)
     grp.barrier()
     t_wall = time.time()
     t = time.perf_counter()
@@ -698,7 +719,8 @@ def c4_block(args, ctx, grp, search, n):
     want = golden(msg, lo, hi)
     out = {"workload": desc, "lower": lo, "upper": hi, "nonces": total, "scaling": scaling,
            "GHs": round(total / dt / 1e9, 4), "seconds": round(dt, 4), "result": list(res), "golden": want,
-           "result_ok": None if want is None else list(res) == want, "combine": rec["combine"]}
+           "result_ok": None if want is None else list(res) == want, "combine": rec["combine"],
+           "warm": f"{warm} untimed searches of {4096} nonces, one per digit count, before the timed one"}
     if grp.world > 1:
         starts = grp.gather(t_wall)
         slots = grp.gather({"rank": grp.rank, "nonces": rec["nonces"], "span_ms": round(rec["span_ms"], 3),
@@ -714,6 +736,97 @@ def c4_block(args, ctx, grp, search, n):
                            if i < len(rec["dev_allgather_ms"]) else None}
                           for i, (nn, sp) in enumerate(rec["devices"])]
     return out
+
+
+ONE_PROCESS_TIMEOUT_S = 300  # the one-process C4 child: set-up, warm-up and timed steps over N devices
+
+
+def c4_one_process(args, grp, n):
+    """under torchrun the line measures the rank path, but the Go
+    shim (go/bitcoin/miner/gpu.go: bm_ctx_create(0)) and BASELINE configs[3]
+    ("one miner process driving 8 x MI355X") are ONE process over N devices:
+    bm_ctx_create(N), its per-device submission threads, balance, and
+    ncclCommInitAll + one grouped allgather.  So after the group's C4 step,
+    with every rank idle at a barrier, rank 0 measures C4 that way too: a
+    child process (bench.py --gpus N --config C4, no launcher: the one-process
+    mode), under a time limit of its own so that a failure or hang there
+    cannot cost the line; the ranks wait at the next barrier.  Under a
+    visibility mask that leaves rank 0 fewer than N devices the block is null
+    with the reason; with --rehearse-one-gpu the child runs N slots on GPU 0
+    (host combine; scaling_valid false)."""
+    import subprocess
+    grp.barrier()  # every rank's kernels are idle from here until the next barrier
+    blk = None
+    if grp.rank == 0:
+        try:
+            blk = _c4_one_process_child(args, n)
+        except Exception as e:  # noqa: BLE001 -- reported in the block, never fatal to the line
+            blk = {"skipped": f"{type(e).__name__}: {e}"[:500]}
+    grp.barrier()
+    return blk
+
+
+def _c4_one_process_child(args, n):
+    import subprocess
+    have = device_count()
+    rehearse = args.rehearse_one_gpu
+    if not rehearse and have < n:
+        return {"skipped": f"rank 0 sees {have} of {n} devices (a visibility mask): no one-process context "
+                           f"over {n} GPUs can open"}
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--gpus", str(n), "--config", "C4", "--no-cpu-baseline",
+           "--no-c4", "--clock-seconds", "0", "--steps", "1" if rehearse else "2", "--warmup", "0" if rehearse else "1"]
+    if rehearse:
+        cmd.append("--rehearse-one-gpu")
+    if args.no_balance:
+        cmd.append("--no-balance")
+    env = child_env(os.environ)  # the child is no torchrun rank: the one-process mode (module docstring)
+    t = time.perf_counter()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=ONE_PROCESS_TIMEOUT_S)
+    except subprocess.TimeoutExpired:
+        import signal
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        return {"skipped": f"the one-process child did not finish in {ONE_PROCESS_TIMEOUT_S} s (killed)"}
+    wall = time.perf_counter() - t
+    lines = [ln for ln in out.strip().splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"skipped": f"the one-process child exited {p.returncode}", "stderr_tail": err[-800:]}
+    return one_process_block(json.loads(lines[-1]), n, wall, cmd[2:])
+
+
+def child_env(environ):
+    """The one-process child's environment: the launcher's rank variables
+    dropped (it is no torchrun rank), WORLD_SIZE 1; the rest (visibility
+    masks, BTCMINER_LIB, ...) kept."""
+    env = {k: v for k, v in environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "GROUP_RANK", "ROLE_RANK", "LOCAL_WORLD_SIZE", "ROLE_WORLD_SIZE",
+                        "GROUP_WORLD_SIZE") and not k.startswith("TORCHELASTIC_")}
+    env["WORLD_SIZE"] = "1"
+    return env
+
+
+def one_process_block(line, n, wall, args):
+    """The c4_one_process block from the one-process child's bench line."""
+    cfg = line["config"]
+    blk = {"design": f"one process, {n} devices: bm_ctx_create({n}), a submission thread per device, "
+                     "balance, ncclCommInitAll + one grouped allgather (go/bitcoin/miner/gpu.go; BASELINE configs[3])",
+           "workload": cfg["workload"], "lower": cfg["lower"], "upper": cfg["upper"], "nonces": cfg["global_nonces"],
+           "GHs": line["value"], "seconds": round(line["ms_per_step"] / 1e3, 4), "steps": line["steps"],
+           "warmup": line["warmup"], "result": line["result"], "golden": line["golden"],
+           "result_ok": line["result_ok"], "parallelism": cfg["parallelism"], "split": cfg["split"],
+           "devices": cfg.get("devices"), "rccl_nranks": line.get("rccl_nranks"),
+           "scaling_valid": line.get("scaling_valid"), "rccl": line.get("rccl"),
+           "start_skew_ms": line.get("start_skew_ms"), "start_threads": line.get("start_threads"),
+           "child_wall_s": round(wall, 2), "child_cmd": " ".join(args)}
+    for k in ("scaling_invalid", "rccl_absent", "rehearsal"):
+        if k in line:
+            blk[k] = line[k]
+    combines = sorted({d["combine"] for d in cfg.get("devices") or []})
+    blk["combine"] = "/".join(combines) if combines else None
+    return blk
 
 
 def scaling_validity(n, slots, want, rehearsal):
@@ -889,9 +1002,8 @@ def main():
         ops = sum(L.nonces * kernel_compressions(L) for L in launches) * OPS_PER_COMPRESSION
         return res, (dom, ops, st.span_ms, step_record(st))
 
-    for _ in range(args.warmup):
-        step()
-    split = calibrate_split(args, ctx, grp)
+    warm = [step()[1][3] for _ in range(args.warmup)]
+    split = calibrate_split(args, ctx, grp, warm)
     sampler = ClockSampler(dev, period=0.05 if (args.clock_sample if args.clock_sample is not None else n > 1)
                            else None)
     grp.barrier()
@@ -918,6 +1030,9 @@ def main():
     # step, after the clock measurement so that the issue bound's clock is
     # taken right after the headline's steps, as before
     c4 = None if (args.no_c4 or args.config == "C4") else c4_block(args, ctx, grp, search, n)
+    # the same C4 search through ONE process over the N devices
+    # (the Go shim's design), measured by rank 0 while the ranks idle
+    c4_one = c4_one_process(args, grp, n) if (world > 1 and c4 is not None) else None
 
     total = hi - lo + 1
     value = total * args.steps / dt / 1e9
@@ -961,6 +1076,8 @@ def main():
     }
     if c4 is not None:
         out["c4"] = c4
+    if world > 1 and c4 is not None:
+        out["c4_one_process"] = c4_one
     if n > 1:
         # what RCCL itself reported (ncclCommCount / UserRank / CuDevice per
         # rank or device) and whether the line measures N distinct GPUs
@@ -1034,6 +1151,14 @@ def main():
             if clock:
                 pm["box_clock_ghz"] = round(clock, 3)
             pm["hbm_bytes_per_launch"] = pmc.get("hbm_bytes_per_launch")
+            # is the imported pass about the kernel this run
+            # loaded?  Both sides hash the kernel's instruction bytes in the
+            # library's gfx950 code object (codeobj.py)
+            mine_sha = codeobj.kernel_code_sha(_lib.LIB_PATH, dom.p, dom.nbv, dom.pad_block)
+            pm["code_sha"] = pmc.get("code_sha")
+            pm["loaded_code_sha"] = mine_sha
+            pm["same_kernel"] = (None if not (pmc.get("code_sha") and mine_sha)
+                                 else pmc["code_sha"] == mine_sha)
         roof["pmc"] = pm
         # the clock under the dominant kernel on this box: live stamps
         # (s_memtime / s_memrealtime, BM_CLOCK_PROBE builds), else the

@@ -54,6 +54,10 @@ constexpr size_t kCtrStride = 32;  // u64 words per launch: counter [0], clock s
 // shares are the rates scaled so the fastest device gets kShareScale.
 constexpr uint64_t kBalanceMinNonces = 1ull << 30;
 constexpr double kShareScale = 65536.0;
+// A device's start offset (bm_stats_t.dev_start_ms) enters its rate only
+// above host jitter: at least 1 ms and 1% of its span.
+constexpr double kBalanceStartMinMs = 1.0;
+constexpr double kBalanceStartMinFrac = 0.01;
 
 // What each device / rank contributes to the combine: its partial and a
 // status word (a rank that failed the call before the combine still takes
@@ -546,6 +550,21 @@ int enqueue_device(bm_ctx* ctx, int di, std::vector<Launch>& launches, uint32_t&
     return BM_OK;
 }
 
+// f() as a status: an exception (std::bad_alloc from a plan or order vector,
+// anything else a bug) becomes BM_ENOMEM / BM_EINTERNAL instead of leaving
+// the C ABI -- or, on a submission thread, calling std::terminate and taking
+// the host process down.
+template <class F>
+int guarded(F&& f) noexcept {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return BM_ENOMEM;
+    } catch (...) {
+        return BM_EINTERNAL;
+    }
+}
+
 // Stage 2 of a search: every device's work.  A context of several devices
 // submits each device's work from a host thread of its own, so device N-1
 // does not wait for the other devices' ~15 API calls each before it starts
@@ -556,18 +575,19 @@ int enqueue(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches, std::vector
     if (ctx->fault_after == 0) return BM_EINTERNAL;  // test hook (also for a rank with nothing to scan)
     std::atomic<int> enqueued{0};
     ctx->stats.start_threads = 1;
-    if (ndev == 1) return enqueue_device(ctx, 0, launches[0], first[0], enqueued);
+    auto one = [&](int di) { return guarded([&] { return enqueue_device(ctx, di, launches[di], first[di], enqueued); }); };
+    if (ndev == 1) return one(0);
     std::vector<int> rc(ndev, BM_OK);
     std::vector<std::thread> th;
     th.reserve(ndev - 1);
     for (int di = 1; di < ndev; ++di) {
         try {
-            th.emplace_back([&, di] { rc[di] = enqueue_device(ctx, di, launches[di], first[di], enqueued); });
+            th.emplace_back([&, di] { rc[di] = one(di); });
         } catch (const std::system_error&) {  // no thread: this one submits that device's work itself
-            rc[di] = enqueue_device(ctx, di, launches[di], first[di], enqueued);
+            rc[di] = one(di);
         }
     }
-    rc[0] = enqueue_device(ctx, 0, launches[0], first[0], enqueued);
+    rc[0] = one(0);
     for (auto& t : th) t.join();
     ctx->stats.start_threads = 1 + (int)th.size();
     for (int r : rc)
@@ -911,7 +931,7 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
     // so the context stays usable.
     std::vector<std::vector<Launch>> launches(ndev);
     std::vector<uint32_t> first(ndev, 0);
-    int rc = plan_launches(ctx, msg, len, lower, upper, launches);
+    int rc = guarded([&] { return plan_launches(ctx, msg, len, lower, upper, launches); });
     if (rc == BM_OK) rc = enqueue(ctx, launches, first);
     if (rc != BM_OK) drain(ctx);
 
@@ -959,7 +979,12 @@ int search_impl(bm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lower, uin
             float ms = 0.f;
             ok = d.piece_nonces >= kBalanceMinNonces && hipSetDevice(d.id) == hipSuccess &&
                  hipEventElapsedTime(&ms, d.bal[0], d.bal[1]) == hipSuccess && ms > 0.f;
-            if (ok) rate[di] = (double)d.piece_nonces / (start_ms[di] + ms);
+            // a start offset counts only when it is more than host jitter
+            // (thread scheduling: sub-ms to ms on a loaded host), so shares
+            // move only for a persistent late start
+            const double late = start_ms[di] >= std::max(kBalanceStartMinMs, kBalanceStartMinFrac * ms) ? start_ms[di]
+                                                                                                          : 0.0;
+            if (ok) rate[di] = (double)d.piece_nonces / (late + ms);
         }
         if (ok) {
             const double top = *std::max_element(rate.begin(), rate.end());
@@ -1361,7 +1386,7 @@ int bm_search_gpu(bm_ctx_t* ctx, const uint8_t* msg, size_t len, uint64_t lower,
     if (!ctx || !out || (len && !msg) || len > BM_MAX_MSG_LEN) return BM_EINVAL;
     bm::DeviceGuard guard;
     bm_result_t r;
-    int rc = bm::search_impl(ctx, msg, len, lower, upper, &r);
+    int rc = bm::guarded([&] { return bm::search_impl(ctx, msg, len, lower, upper, &r); });
     if (rc == BM_OK) *out = r;
     return rc;
 }

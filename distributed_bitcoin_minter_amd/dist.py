@@ -62,6 +62,37 @@ def shares_from_rates(rates):
     return [max(1, math.floor(r / top * SHARE_SCALE + 0.5)) for r in rates]
 
 
+def _median(xs):
+    ys = sorted(xs)
+    m = len(ys) // 2
+    return ys[m] if len(ys) % 2 else (ys[m - 1] + ys[m]) / 2
+
+
+def calibrated_rates(per_rank, bound=0.85, agree=0.02):
+    """One rate per rank from the rates of its warmup steps (nonces per ms,
+    each step after a process's first, which loads the code objects), robust
+    to one transient step (a clock ramp or a late code-object load
+    in the one step used before fixed a skewed split for every timed step):
+      * each rank's rate is the median of its steps;
+      * a rank below `bound` of the fastest rank is held at `bound` of it,
+        unless two of its steps agree within `agree` that it really is that
+        slow (a persistently slower GPU keeps its measured rate).
+    Returns (rates, info): info["clamped"] lists the ranks held at the bound,
+    info["spread"] each rank's (max - min) / max over its steps."""
+    med = [_median(r) for r in per_rank]
+    top = max(med)
+    rates, clamped = [], []
+    for i, (r, m) in enumerate(zip(per_rank, med)):
+        if m < bound * top:
+            low = sorted(x for x in r if x < bound * top)
+            if not any(b - a <= agree * b for a, b in zip(low, low[1:])):
+                m = bound * top
+                clamped.append(i)
+        rates.append(m)
+    spread = [round((max(r) - min(r)) / max(r), 4) if max(r) > 0 else 0.0 for r in per_rank]
+    return rates, {"clamped": clamped, "spread": spread}
+
+
 def lex_min(pairs):
     """Lexicographic (hash, nonce) min; (2^64-1, 2^64-1) for no pairs."""
     best = (U64_MAX, U64_MAX)

@@ -39,6 +39,21 @@ and a new request gets slots as soon as the next ones free up instead of
 waiting for earlier requests to drain.  Chunks of one request are issued in
 ascending order.
 
+Chunk size per miner (round 6).  A fixed chunk does not fit every miner: a
+miner driving 8 GPUs (the Go shim's default, bm_ctx_create(0)) finishes a
+2^32-nonce job in about 10 ms, most of it per-call cost.  So ``chunk`` is the
+BASE size, and each miner's jobs are a multiple of it sized from the miner's
+own measured rate (``chunk_for``): about ``target_ms`` of its work per job
+(default 300 ms), at most ``max_mult`` bases (default 64), at most twice the
+miner's previous multiple (a ramp, so one odd sample cannot jump the size),
+and at most the miner's rate-proportional share of what the request has left
+(so a fast miner does not take a short request's whole tail while slower
+miners idle).  The rate is the median of the miner's last 5 jobs, each its
+nonces over the time from when the miner could start it (its send, or the
+previous result if that came later) to its result.  A new miner gets one
+base.  ``target_ms = 0`` keeps the fixed chunk.  The wire format is
+unchanged: a Request's [Lower, Upper] is just wider.
+
 Job queue depth.  Each miner holds up to ``depth`` jobs (default 2; the
 reference's one-job-per-miner is depth 1).  A miner works through its jobs in
 order (LSP delivers in order), so when a GPU finishes a chunk the next one is
@@ -55,12 +70,31 @@ import argparse
 import collections
 import itertools
 import sys
+import time
 
 from . import lsp
 from .bitcoin import Message, MsgType, NewRequest, NewResult, U64_MAX
 
 DEFAULT_CHUNK = 1 << 32
 DEFAULT_DEPTH = 2
+DEFAULT_TARGET_MS = 300   # per-miner job time the chunk sizing aims at
+DEFAULT_MAX_MULT = 64     # largest job, in base chunks
+RATE_SAMPLES = 5          # a miner's rate: the median of its last jobs
+
+
+def chunk_for(base, target_s, max_mult, rate, prev_mult, remaining, share):
+    """Multiple of `base` nonces for a miner's next job (module docstring):
+    rate (nonces/s, None before the miner's first result) x target_s, rounded,
+    in [1, max_mult], at most 2 x prev_mult, and at most the miner's `share`
+    (its fraction of all miners' rates) of the request's `remaining` nonces,
+    rounded up to a base.  Returns the multiple k >= 1."""
+    if target_s <= 0 or not rate:
+        return 1
+    k = int(rate * target_s / base + 0.5)
+    k = max(1, min(k, max_mult, 2 * max(1, prev_mult)))
+    if 0 < share < 1:
+        k = min(k, max(1, -(-int(remaining * share) // base)))
+    return k
 
 
 class _Request:
@@ -108,14 +142,21 @@ class BitcoinServer:
     """Owns an ``lsp.Server``; ``serve()`` runs the event loop until the LSP
     server is closed (``close()`` from another thread ends it)."""
 
-    def __init__(self, lsp_server, chunk=DEFAULT_CHUNK, depth=DEFAULT_DEPTH, log=None):
-        if chunk < 1 or depth < 1:
-            raise ValueError("chunk and depth must be >= 1")
+    def __init__(self, lsp_server, chunk=DEFAULT_CHUNK, depth=DEFAULT_DEPTH, log=None, target_ms=DEFAULT_TARGET_MS,
+                 max_mult=DEFAULT_MAX_MULT, clock=time.monotonic):
+        if chunk < 1 or depth < 1 or target_ms < 0 or max_mult < 1:
+            raise ValueError("chunk, depth and max_mult must be >= 1, target_ms >= 0")
         self.srv = lsp_server
         self.chunk = int(chunk)
         self.depth = int(depth)
+        self.target_s = target_ms / 1e3
+        self.max_mult = int(max_mult)
+        self.clock = clock
         self.log = log or (lambda *a: None)
-        self.miners = {}                    # conn id -> deque of (request id, lo, hi) sent, oldest first
+        self.miners = {}                    # conn id -> deque of (request id, lo, hi, sent at) sent, oldest first
+        self.rates = {}                     # conn id -> deque of its last jobs' rates (nonces/s)
+        self._mult = {}                     # conn id -> multiple of its last fresh chunk
+        self._last_done = {}                # conn id -> time of its last result
         self._free_since = {}               # conn id -> tick at which its job count last dropped
         self._tick = itertools.count()
         self.requests = collections.OrderedDict()  # rid -> _Request, oldest first
@@ -148,6 +189,9 @@ class BitcoinServer:
         if msg.Type == MsgType.Join:
             if cid not in self.miners:
                 self.miners[cid] = collections.deque()
+                self.rates[cid] = collections.deque(maxlen=RATE_SAMPLES)
+                self._mult[cid] = 0
+                self._last_done[cid] = None
                 self._free_since[cid] = next(self._tick)
                 self.stats["joins"] += 1
         elif msg.Type == MsgType.Request:
@@ -163,8 +207,16 @@ class BitcoinServer:
             if not jobs:
                 return  # not a miner, or a miner with no job: stray
             # a miner answers its jobs in the order it got them (LSP delivers in order)
-            rid, lo, hi = jobs.popleft()
+            rid, lo, hi, sent = jobs.popleft()
             self._free_since[cid] = next(self._tick)
+            # its rate on this job: from when it could start it (sent, or
+            # its previous result if that came later) to this result
+            now = self.clock()
+            prev = self._last_done.get(cid)
+            start = sent if prev is None else max(sent, prev)
+            self._last_done[cid] = now
+            if now > start:
+                self.rates[cid].append((hi - lo + 1) / (now - start))
             r = self.requests.get(rid)
             if r is not None:  # None: its client is gone, ignore (README:414)
                 r.inflight -= 1
@@ -177,8 +229,10 @@ class BitcoinServer:
         if cid in self.miners:
             jobs = self.miners.pop(cid)
             self._free_since.pop(cid, None)
+            for d in (self.rates, self._mult, self._last_done):
+                d.pop(cid, None)
             self.stats["miners_lost"] += 1
-            for rid, lo, hi in reversed(jobs):  # README:413: reassign, lowest chunk first
+            for rid, lo, hi, _sent in reversed(jobs):  # README:413: reassign, lowest chunk first
                 r = self.requests.get(rid)
                 if r is not None:
                     r.inflight -= 1
@@ -210,6 +264,28 @@ class BitcoinServer:
                     best, key = m, k
         return best
 
+    def rate(self, mid):
+        """The miner's measured rate (nonces/s): median of its last jobs, or None."""
+        xs = sorted(self.rates.get(mid) or ())
+        if not xs:
+            return None
+        m = len(xs) // 2
+        return xs[m] if len(xs) % 2 else (xs[m - 1] + xs[m]) / 2
+
+    def chunk_size(self, mid, r):
+        """Nonces of miner mid's next fresh chunk of request r (chunk_for)."""
+        rate = self.rate(mid)
+        if self.target_s <= 0 or rate is None:
+            k = 1
+        else:
+            known = [x for x in (self.rate(m) for m in self.miners) if x]
+            total = sum(self.rate(m) or (sum(known) / len(known)) for m in self.miners)
+            remaining = r.upper - r.next_lower + 1 if not r.done else 0
+            k = chunk_for(self.chunk, self.target_s, self.max_mult, rate, self._mult.get(mid, 0), remaining,
+                          rate / total if total > 0 else 1.0)
+        self._mult[mid] = k
+        return k * self.chunk
+
     def _schedule(self):
         while True:
             mid = self._free_miner()
@@ -218,7 +294,7 @@ class BitcoinServer:
             r = self._pick()
             if r is None:
                 return
-            lo, hi = r.take(self.chunk)
+            lo, hi = r.take(self.chunk if r.retry else self.chunk_size(mid, r))
             try:
                 self.srv.Write(mid, NewRequest(r.data, lo, hi).marshal())
             except lsp.LSPError:
@@ -227,9 +303,10 @@ class BitcoinServer:
                 r.retry.appendleft((lo, hi))
                 self._on_lost(mid)
                 return
-            self.miners[mid].append((r.rid, lo, hi))
+            self.miners[mid].append((r.rid, lo, hi, self.clock()))
             r.inflight += 1
             self.stats["chunks_sent"] += 1
+            self.stats["nonces_sent"] += hi - lo + 1
 
     def _maybe_finish(self, r):
         if not r.finished():
@@ -258,7 +335,11 @@ def main(argv=None):
     """``server <port>`` (README:365-368)."""
     ap = argparse.ArgumentParser(prog="server", description="bitcoin mining server (LSP)")
     ap.add_argument("port", type=int)
-    ap.add_argument("--chunk", type=int, default=DEFAULT_CHUNK, help="nonces per miner job (default 2^32)")
+    ap.add_argument("--chunk", type=int, default=DEFAULT_CHUNK,
+                    help="base nonces per miner job (default 2^32); jobs are multiples of it sized by each miner's rate")
+    ap.add_argument("--target-ms", type=int, default=DEFAULT_TARGET_MS,
+                    help="per-miner job time the sizing aims at (default 300 ms; 0: every job is one base chunk)")
+    ap.add_argument("--max-mult", type=int, default=DEFAULT_MAX_MULT, help="largest job in base chunks (default 64)")
     ap.add_argument("--depth", type=int, default=DEFAULT_DEPTH,
                     help="jobs queued per miner (default 2: the next job is already there when one ends)")
     ap.add_argument("--epoch-limit", type=int, default=lsp.DefaultEpochLimit)
@@ -273,7 +354,7 @@ def main(argv=None):
         print(f"Failed to start server: {e}", file=sys.stderr)
         return 1
     log = (lambda *x: print(*x, file=sys.stderr, flush=True)) if a.v else None
-    s = BitcoinServer(srv, chunk=a.chunk, depth=a.depth, log=log)
+    s = BitcoinServer(srv, chunk=a.chunk, depth=a.depth, log=log, target_ms=a.target_ms, max_mult=a.max_mult)
     try:
         s.serve()
     except KeyboardInterrupt:

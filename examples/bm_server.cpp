@@ -1,7 +1,7 @@
 // bm_server.cpp -- the bitcoin server (range scheduler) in C++ on lsp.hpp.
 //
-//   bm_server port [--chunk N] [--depth D] [--epoch-limit K] [--epoch-millis MS]
-//             [--window-size W] [--host ADDR] [--drop-read P] [--drop-write P] [-v]
+//   bm_server port [--chunk N] [--depth D] [--target-ms T] [--max-mult M] [--epoch-limit K]
+//             [--epoch-millis MS] [--window-size W] [--host ADDR] [--drop-read P] [--drop-write P] [-v]
 //
 // The C++ twin of distributed_bitcoin_minter_amd/server.py (whose docstring
 // states the design) for bitcoin/server/server.go and README:341-417:
@@ -9,6 +9,10 @@
 //   * the inclusive range is cut into chunks of --chunk nonces (default 2^32,
 //     retuned from server.go:18's minerLoad = 24 for GPU miners), handed to
 //     miners with free job slots (each holds up to --depth jobs, default 2);
+//   * each miner's chunks are a multiple of --chunk sized from its measured
+//     rate (server.py chunk_for): about --target-ms of its work (default 300;
+//     0 = fixed chunks), at most --max-mult bases (64), at most twice its
+//     previous multiple, at most its rate share of the request's remainder;
 //   * fair share: the next chunk goes to the active request with the fewest
 //     chunks in flight (oldest on ties), to the miner with the fewest queued
 //     jobs (longest-free on ties);
@@ -18,9 +22,13 @@
 //     lost client's requests are dropped; a client's results go out in the
 //     order it sent its requests.
 // With port 0 the chosen port is printed first ("port <n>").  No GPU needed.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <vector>
 #include <map>
 #include <memory>
 #include <string>
@@ -62,15 +70,49 @@ struct Request {
     }
 };
 
+using Clock = std::chrono::steady_clock;
+
 struct Job {
     uint64_t rid;
     Range r;
+    Clock::time_point sent;
 };
+
+// A miner's measured rate: its last jobs' nonces per second (server.py RATE_SAMPLES).
+struct MinerRate {
+    std::deque<double> samples;
+    uint64_t mult = 0;  // multiple of its last fresh chunk
+    bool have_done = false;
+    Clock::time_point last_done;
+    double rate() const {  // median, 0 before the first result
+        if (samples.empty()) return 0.0;
+        std::vector<double> v(samples.begin(), samples.end());
+        std::sort(v.begin(), v.end());
+        const size_t m = v.size() / 2;
+        return v.size() % 2 ? v[m] : (v[m - 1] + v[m]) / 2;
+    }
+};
+constexpr size_t kRateSamples = 5;
+
+// server.py chunk_for: the multiple k >= 1 of `base` for a miner's next job.
+uint64_t chunk_for(uint64_t base, double target_s, uint64_t max_mult, double rate, uint64_t prev_mult,
+                   uint64_t remaining, double share) {
+    if (target_s <= 0 || rate <= 0) return 1;
+    const double want = std::floor(rate * target_s / (double)base + 0.5);
+    uint64_t k = want >= (double)max_mult ? max_mult : (uint64_t)std::max(1.0, want);
+    k = std::max<uint64_t>(1, std::min({k, max_mult, 2 * std::max<uint64_t>(1, prev_mult)}));
+    if (share > 0 && share < 1) {
+        const double mine = std::floor((double)remaining * share);
+        const uint64_t cap = (uint64_t)std::ceil(mine / (double)base);
+        k = std::min(k, std::max<uint64_t>(1, cap));
+    }
+    return k;
+}
 
 class BitcoinServer {
    public:
-    BitcoinServer(lsp::Server& srv, uint64_t chunk, size_t depth, bool verbose)
-        : srv_(srv), chunk_(chunk), depth_(depth), verbose_(verbose) {}
+    BitcoinServer(lsp::Server& srv, uint64_t chunk, size_t depth, double target_s, uint64_t max_mult, bool verbose)
+        : srv_(srv), chunk_(chunk), depth_(depth), target_s_(target_s), max_mult_(max_mult), verbose_(verbose) {}
 
     void serve() {
         for (;;) {
@@ -97,6 +139,7 @@ class BitcoinServer {
             case bitcoin::MsgType::Join:
                 if (!miners_.count(cid)) {
                     miners_[cid];
+                    rates_[cid];
                     free_since_[cid] = tick_++;
                     if (verbose_) std::fprintf(stderr, "miner %lld joined\n", (long long)cid);
                 }
@@ -115,6 +158,18 @@ class BitcoinServer {
                 const Job j = mi->second.front();  // a miner answers in the order it got its jobs
                 mi->second.pop_front();
                 free_since_[cid] = tick_++;
+                // its rate on this job: from when it could start it (sent, or its
+                // previous result if that came later) to this result
+                MinerRate& mr = rates_[cid];
+                const auto now = Clock::now();
+                const auto start = mr.have_done ? std::max(j.sent, mr.last_done) : j.sent;
+                mr.last_done = now;
+                mr.have_done = true;
+                const double secs = std::chrono::duration<double>(now - start).count();
+                if (secs > 0) {
+                    mr.samples.push_back((double)(j.r.second - j.r.first + 1) / secs);
+                    if (mr.samples.size() > kRateSamples) mr.samples.pop_front();
+                }
                 auto ri = requests_.find(j.rid);
                 if (ri != requests_.end()) {  // else its client is gone (README:414)
                     Request& r = ri->second;
@@ -140,6 +195,7 @@ class BitcoinServer {
             }
             miners_.erase(mi);
             free_since_.erase(cid);
+            rates_.erase(cid);
             if (verbose_) std::fprintf(stderr, "miner %lld lost\n", (long long)cid);
         } else {
             auto ci = client_reqs_.find(cid);
@@ -172,13 +228,34 @@ class BitcoinServer {
         return best;
     }
 
+    // Nonces of miner mid's next fresh chunk of r (chunk_for).
+    uint64_t chunk_size(int64_t mid, const Request& r) {
+        MinerRate& mr = rates_[mid];
+        const double rate = mr.rate();
+        uint64_t k = 1;
+        if (target_s_ > 0 && rate > 0) {
+            double known = 0, total = 0;
+            size_t nk = 0;
+            for (const auto& kv : rates_)
+                if (kv.second.rate() > 0) {
+                    known += kv.second.rate();
+                    ++nk;
+                }
+            for (const auto& kv : rates_) total += kv.second.rate() > 0 ? kv.second.rate() : known / (double)nk;
+            const uint64_t remaining = r.done ? 0 : r.upper - r.next_lower + 1;  // wraps only for all 2^64
+            k = chunk_for(chunk_, target_s_, max_mult_, rate, mr.mult, remaining, total > 0 ? rate / total : 1.0);
+        }
+        mr.mult = k;
+        return k > UINT64_MAX / chunk_ ? UINT64_MAX : k * chunk_;
+    }
+
     void schedule() {
         for (;;) {
             const int64_t mid = free_miner();
             if (!mid) return;
             Request* r = pick();
             if (!r) return;
-            const Range c = r->take(chunk_);
+            const Range c = r->take(r->retry.empty() ? chunk_size(mid, *r) : chunk_);
             try {
                 srv_.Write(mid, bitcoin::NewRequest(r->data, c.first, c.second).Marshal());
             } catch (const lsp::LSPError&) {  // miner already gone (server.go:177-179)
@@ -186,7 +263,7 @@ class BitcoinServer {
                 on_lost(mid);
                 return;
             }
-            miners_[mid].push_back(Job{r->rid, c});
+            miners_[mid].push_back(Job{r->rid, c, Clock::now()});
             ++r->inflight;
         }
     }
@@ -213,7 +290,10 @@ class BitcoinServer {
     lsp::Server& srv_;
     const uint64_t chunk_;
     const size_t depth_;
+    const double target_s_;
+    const uint64_t max_mult_;
     const bool verbose_;
+    std::map<int64_t, MinerRate> rates_;
     std::map<int64_t, std::deque<Job>> miners_;  // conn id -> jobs sent, oldest first
     std::map<int64_t, uint64_t> free_since_;
     uint64_t tick_ = 0, next_rid_ = 1;
@@ -223,7 +303,8 @@ class BitcoinServer {
 
 [[noreturn]] void usage(const char* argv0) {
     std::fprintf(stderr,
-                 "usage: %s port [--chunk N] [--depth D] [--epoch-limit K] [--epoch-millis MS] [--window-size W]\n"
+                 "usage: %s port [--chunk N] [--depth D] [--target-ms T] [--max-mult M] [--epoch-limit K]\n"
+                 "          [--epoch-millis MS] [--window-size W]\n"
                  "          [--host ADDR] [--drop-read P] [--drop-write P] [-v]\n",
                  argv0);
     std::exit(1);
@@ -234,7 +315,7 @@ class BitcoinServer {
 int main(int argc, char** argv) {
     lsp::Params p;
     uint64_t chunk = 1ull << 32;
-    long long depth = 2;
+    long long depth = 2, target_ms = 300, max_mult = 64;
     int port = -1;
     std::string host = "127.0.0.1";
     bool verbose = false;
@@ -246,6 +327,8 @@ int main(int argc, char** argv) {
         };
         if (a == "--chunk") chunk = std::strtoull(val(), nullptr, 10);
         else if (a == "--depth") depth = std::atoll(val());
+        else if (a == "--target-ms") target_ms = std::atoll(val());
+        else if (a == "--max-mult") max_mult = std::atoll(val());
         else if (a == "--epoch-limit") p.EpochLimit = std::atoi(val());
         else if (a == "--epoch-millis") p.EpochMillis = std::atoi(val());
         else if (a == "--window-size") p.WindowSize = std::atoi(val());
@@ -256,7 +339,7 @@ int main(int argc, char** argv) {
         else if (port < 0 && !a.empty() && a[0] != '-') port = std::atoi(a.c_str());
         else usage(argv[0]);
     }
-    if (port < 0 || chunk < 1 || depth < 1) usage(argv[0]);
+    if (port < 0 || chunk < 1 || depth < 1 || target_ms < 0 || max_mult < 1) usage(argv[0]);
     std::unique_ptr<lsp::Server> srv;
     try {
         srv = lsp::NewServer(port, p, host);
@@ -268,6 +351,6 @@ int main(int argc, char** argv) {
         std::printf("port %d\n", srv->port());
         std::fflush(stdout);
     }
-    BitcoinServer(*srv, chunk, (size_t)depth, verbose).serve();
+    BitcoinServer(*srv, chunk, (size_t)depth, (double)target_ms / 1e3, (uint64_t)max_mult, verbose).serve();
     return 0;
 }

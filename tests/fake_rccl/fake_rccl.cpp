@@ -72,32 +72,44 @@ struct ncclComm {
     Shared* sh = nullptr;
     std::atomic<bool> aborted{false};
     uint64_t seq = 0;       // allgathers enqueued so far
-    uint64_t target = 0;    // the call the pending host function serves
-    size_t bytes = 0;       // its per-rank size
+    // pinned staging buffers: reused call after call, which is safe because
+    // one communicator's calls run in the order of its one stream
     uint8_t* h_send = nullptr;
     uint8_t* h_recv = nullptr;
 };
 
 namespace {
+// What one allgather's host function needs, fixed when the call is enqueued
+// (held on the communicator, a second call enqueued before the
+// first's host function ran would have made both use the second's seq).
+struct Call {
+    ncclComm* c;
+    uint64_t seq;
+    size_t bytes;
+};
+
 // The host function of one allgather (runs in stream order, after the D2H
-// copy of this rank's bytes).  No HIP calls in here.
+// copy of this rank's bytes).  No HIP calls in here.  Frees its Call.
 void exchange(void* p) {
-    ncclComm* c = static_cast<ncclComm*>(p);
-    const uint64_t s = c->target;
+    Call* call = static_cast<Call*>(p);
+    ncclComm* c = call->c;
+    const uint64_t s = call->seq;
+    const size_t bytes = call->bytes;
+    delete call;
     const int b = (int)(s & 1);
     Slot& mine = c->sh->slot[c->rank];
-    std::memcpy(mine.data[b], c->h_send, c->bytes);
+    std::memcpy(mine.data[b], c->h_send, bytes);
     mine.seq[b].store(s, std::memory_order_release);
     for (int r = 0; r < c->nranks; ++r) {
         Slot& o = c->sh->slot[r];
         while (o.seq[b].load(std::memory_order_acquire) < s) {
             if (c->aborted.load()) {
-                std::memset(c->h_recv, 0xFF, c->bytes * (size_t)c->nranks);
+                std::memset(c->h_recv, 0xFF, bytes * (size_t)c->nranks);
                 return;
             }
             std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
-        std::memcpy(c->h_recv + (size_t)r * c->bytes, o.data[b], c->bytes);
+        std::memcpy(c->h_recv + (size_t)r * bytes, o.data[b], bytes);
     }
 }
 }  // namespace
@@ -196,11 +208,16 @@ ncclResult_t ncclAllGather(const void* send, void* recv, size_t count, ncclDataT
     const size_t bytes = count * type_bytes(type);
     if (bytes == 0 || bytes > kMaxBytes) return ncclInvalidArgument;
     if (c->aborted.load()) return ncclInvalidUsage;
-    c->bytes = bytes;
-    c->target = ++c->seq;
-    if (hipMemcpyAsync(c->h_send, send, bytes, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        hipLaunchHostFunc(stream, exchange, c) != hipSuccess ||
-        hipMemcpyAsync(recv, c->h_recv, bytes * (size_t)c->nranks, hipMemcpyHostToDevice, stream) != hipSuccess)
+    Call* call = new Call{c, ++c->seq, bytes};
+    if (hipMemcpyAsync(c->h_send, send, bytes, hipMemcpyDeviceToHost, stream) != hipSuccess) {
+        delete call;
+        return ncclUnhandledCudaError;
+    }
+    if (hipLaunchHostFunc(stream, exchange, call) != hipSuccess) {
+        delete call;  // never queued: nobody else frees it
+        return ncclUnhandledCudaError;
+    }
+    if (hipMemcpyAsync(recv, c->h_recv, bytes * (size_t)c->nranks, hipMemcpyHostToDevice, stream) != hipSuccess)
         return ncclUnhandledCudaError;
     return ncclSuccess;
 }

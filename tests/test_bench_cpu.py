@@ -354,8 +354,11 @@ def test_c4_block_one_process_and_ranks():
     want = bench.golden(b"bradfitz", 0, 2 ** 40 - 1)
 
     class Ctx:
+        calls = []
+
         def search(self, msg, lo, hi):
-            assert (msg, lo, hi) == (b"bradfitz", 0, 2 ** 40 - 1)
+            self.calls.append((lo, hi))
+            assert msg == b"bradfitz" and 0 <= lo <= hi <= 2 ** 40 - 1
             return tuple(want)
 
         def last_stats(self):
@@ -368,9 +371,68 @@ def test_c4_block_one_process_and_ranks():
 
     ctx = Ctx()
     c4 = bench.c4_block(NS(), ctx, bench.Group(), ctx.search, 2)
+    # one tiny untimed search at the start of each of the 13 digit
+    # counts first (every C4 layout loaded), then the timed whole range
+    assert ctx.calls[-1] == (0, 2 ** 40 - 1) and len(ctx.calls) == 14, ctx.calls
+    assert ctx.calls[:2] == [(0, 4095), (10, 4105)] and ctx.calls[12] == (10 ** 12, 10 ** 12 + 4095)
+    assert c4["warm"].startswith("13 untimed searches")
     assert (c4["lower"], c4["upper"], c4["nonces"], c4["scaling"]) == (0, 2 ** 40 - 1, 2 ** 40, "strong")
     assert c4["result_ok"] is True and c4["result"] == want and c4["combine"] == "host"
     assert [d["nonces"] for d in c4["devices"]] == [2 ** 39, 2 ** 39] and c4["devices"][1]["start_ms"] == 0.05
     assert c4["GHs"] > 0 and c4["seconds"] >= 0
     # the step record keeps the timed call's launch count (the line's call roofline uses it)
     assert bench.step_record(ctx.last_stats())["launches"] == 14
+
+
+def test_c4_one_process_block_pieces(monkeypatch):
+    """under torchrun, rank 0 measures C4 once more through ONE
+    process over the N devices (a child bench.py in the one-process mode).
+    On CPU: the child's environment drops the launcher's rank variables; a
+    visibility mask that leaves rank 0 fewer than N devices skips the block
+    with the reason; the block carries what the verdict asks for from the
+    child's line (GH/s, result_ok, per-device nonces / span / start /
+    allgather, the combine, rccl_nranks, scaling_valid)."""
+    from types import SimpleNamespace as NS
+    env = bench.child_env({"RANK": "3", "LOCAL_RANK": "3", "WORLD_SIZE": "8", "TORCHELASTIC_RUN_ID": "x",
+                           "LOCAL_WORLD_SIZE": "8", "HIP_VISIBLE_DEVICES": "0,1", "BTCMINER_LIB": "/l.so"})
+    assert env == {"WORLD_SIZE": "1", "HIP_VISIBLE_DEVICES": "0,1", "BTCMINER_LIB": "/l.so"}, env
+    monkeypatch.setattr(bench, "device_count", lambda: 1)
+    blk = bench._c4_one_process_child(NS(rehearse_one_gpu=False, no_balance=False), 2)
+    assert "rank 0 sees 1 of 2 devices" in blk["skipped"], blk
+    devs = [{"device": i, "pci_bus_id": f"0000:{0x20 + i:02x}:00.0", "nonces": 2 ** 39, "span_ms": 9900.0 + i,
+             "GHs": 55.5, "combine": "rccl", "rccl_nranks": 2, "rccl_rank": i, "rccl_device": i,
+             "start_ms": 0.01 * i, "allgather_ms": 0.05, "rccl_init_ms": 310.0, "combine_ms": 0.1} for i in range(2)]
+    line = {"value": 110.6, "ms_per_step": 9941.0, "steps": 2, "warmup": 1, "result": [16555811, 890536971553],
+            "golden": [16555811, 890536971553], "result_ok": True, "rccl_nranks": 2, "scaling_valid": True,
+            "rccl": {"version": 22703}, "start_skew_ms": 0.01, "start_threads": 2,
+            "config": {"workload": "C4: ...", "lower": 0, "upper": 2 ** 40 - 1, "global_nonces": 2 ** 40,
+                       "parallelism": "one process, 2 devices; combine rccl", "devices": devs,
+                       "split": {"mode": "measured device rates (bm_ctx_set_balance)", "shares": [65536, 65400]}}}
+    blk = bench.one_process_block(line, 2, 25.3, ["--gpus", "2", "--config", "C4"])
+    assert blk["GHs"] == 110.6 and blk["result_ok"] is True and blk["combine"] == "rccl", blk
+    assert blk["rccl_nranks"] == 2 and blk["scaling_valid"] is True and blk["seconds"] == 9.941
+    assert [d["nonces"] for d in blk["devices"]] == [2 ** 39] * 2 and blk["devices"][1]["start_ms"] == 0.01
+    assert "bm_ctx_create(2)" in blk["design"] and blk["child_cmd"] == "--gpus 2 --config C4"
+    assert "scaling_invalid" not in blk and blk["split"]["shares"] == [65536, 65400]
+
+
+def test_pmc_same_kernel_code_hash():
+    """an imported PMC summary is tied to the kernel it profiled
+    by the sha256 of that kernel's instruction bytes in the library's gfx950
+    code object (codeobj.py); distinct layouts hash differently, the same
+    library twice the same, the clock-probe build (other instructions) not."""
+    import pytest
+    from distributed_bitcoin_minter_amd import codeobj
+    lib = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "libbtcminer.so")
+    if not os.path.exists(lib):
+        pytest.skip("library not built")
+    c2 = codeobj.kernel_code_sha(lib, 18, 1)
+    assert c2 and len(c2) == 64 and c2 == codeobj.kernel_code_sha(lib, 18, 1)
+    shas = {codeobj.kernel_code_sha(lib, *k) for k in [(18, 1, 0), (12, 1, 0), (60, 1, 2), (60, 1, 3), (60, 1, 4),
+                                                        (13, 2, 0)]}
+    assert None not in shas and len(shas) == 6
+    assert codeobj.kernel_code_sha(lib, 99, 1) is None
+    assert codeobj.mangled_prefix(60, 1, 4) == "_ZN2bm18search_kernel_padkILi60ELi2ELi1EEE"
+    probe = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "libbtcminer_probe.so")
+    if os.path.exists(probe):
+        assert codeobj.kernel_code_sha(probe, 18, 1) not in (None, c2)

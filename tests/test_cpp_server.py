@@ -237,3 +237,42 @@ def test_vanished_miner_chunk_is_reassigned(oracle):
         assert got["r"] == oracle.search(b"failover", 0, 1999)
     finally:
         srv.kill()
+
+
+class _Paced:
+    """A CPU miner's searcher whose time is proportional to its nonces."""
+
+    def __init__(self, oracle, rate):
+        self.oracle, self.rate, self.jobs = oracle, rate, []
+
+    def search(self, data, lower, upper):
+        self.jobs.append((lower, upper))
+        time.sleep((upper - lower + 1) / self.rate)
+        return self.oracle.search(_as_bytes(data), lower, upper)
+
+
+@pytest.mark.parametrize("target_ms", [0, 200])
+def test_rate_sized_chunks(oracle, target_ms):
+    """Round 6: bm_server sizes each miner's jobs from its
+    measured rate like server.py (chunk_for).  Two paced miners, one 8x
+    faster: with --target-ms 200 the fast one's median job is about 8x the
+    slow one's; with --target-ms 0 every job is one --chunk.  The answer is
+    the sequential scan's either way."""
+    p, flags = _params(ms=20, k=100)
+    srv = Proc([_server(), "0", "--chunk", "2000", "--target-ms", str(target_ms), *flags])
+    try:
+        fast, slow = _Paced(oracle, 400_000), _Paced(oracle, 50_000)
+        for s in (fast, slow):
+            threading.Thread(target=miner.run, args=(srv.addr, p, s), daemon=True).start()
+        time.sleep(0.3)
+        from distributed_bitcoin_minter_amd import client
+        n = 1_200_000 if target_ms else 200_000
+        assert client.request(srv.addr, "paced", n - 1, p) == oracle.search(b"paced", 0, n - 1)
+        sizes = [sorted(b - a + 1 for a, b in m.jobs) for m in (fast, slow)]
+        if target_ms:
+            ratio = sizes[0][len(sizes[0]) // 2] / sizes[1][len(sizes[1]) // 2]
+            assert 4.0 <= ratio <= 12.0, sizes
+        else:
+            assert max(sizes[0] + sizes[1]) == 2000, sizes
+    finally:
+        srv.kill()

@@ -195,12 +195,18 @@ def test_bench_torchrun_joined_group_line():
     assert rc["version"] == 1 and rc["version_str"] == "0.0.1" and rc["init_ms"] > 0, rc
     assert 0 < rc["allgather_ms_min"] <= rc["allgather_ms_max"], rc
     assert cfg["split"]["mode"].startswith("measured rank rates") and len(cfg["split"]["shares"]) == 2
+    # the median over the warmup steps after the first (here one), with its spread
+    assert "median of warmup steps 2..2" in cfg["split"]["mode"] and len(cfg["split"]["spread"]) == 2
     assert line["start_skew_ms"] >= 0 and all("start_offset_ms" in r for r in ranks)
     assert line["scaling_valid"] is False and line["scaling_invalid"] == [
         "1 distinct GPUs (PCI bus ids) under 2 ranks / devices"], line["scaling_invalid"]
     c4 = line["c4"]
     assert c4["result_ok"] is True and c4["combine"] == "rccl" and c4["nonces"] == 2 ** 40, c4
     assert sum(r["nonces"] for r in c4["ranks"]) == 2 ** 40 and all(r["allgather_ms"] > 0 for r in c4["ranks"])
+    # the one-process C4 block; HIP_VISIBLE_DEVICES=0 leaves rank 0
+    # one of the two devices a one-process context would need: skipped, and why
+    one = line["c4_one_process"]
+    assert "rank 0 sees 1 of 2 devices" in one["skipped"], one
 
 
 _RANK_DIES = r"""

@@ -260,6 +260,23 @@ def test_bench_torchrun_rehearsal():
     assert out["scaling_valid"] is False and "rehearsal" in out["scaling_invalid"][0]
 
 
+def test_bench_torchrun_rehearsal_c4_one_process():
+    """a torchrun line at N > 1 also measures C4 through ONE
+    process over the N devices (the Go shim's and BASELINE configs[3]'s
+    design): rank 0 runs it in a child while the ranks idle.  Rehearsed on
+    one GPU: 2 slots on GPU 0, host combine, the 2^40 golden, and no scaling
+    claim."""
+    out = _line(_bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--rehearse-one-gpu"], torchrun=2))
+    assert out["result_ok"] is True and out["c4"]["result_ok"] is True, out.get("c4")
+    one = out["c4_one_process"]
+    assert "skipped" not in one, one
+    assert one["result_ok"] is True and one["result"] == [16555811, 890536971553] and one["nonces"] == 2 ** 40, one
+    assert one["combine"] == "host" and one["scaling_valid"] is False and one["GHs"] > 10, one
+    assert len(one["devices"]) == 2 and sum(d["nonces"] for d in one["devices"]) == 2 ** 40, one
+    assert all("start_ms" in d and "allgather_ms" in d for d in one["devices"]) and one["start_threads"] == 2
+    assert "bm_ctx_create(2)" in one["design"] and "--rehearse-one-gpu" in one["child_cmd"]
+
+
 def test_bench_torchrun_rccl_world1():
     """bench.py under torchrun at world 1 is the plain path; the RCCL rank
     context at world 1 runs through the rendezvous with --combine rccl when

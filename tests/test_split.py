@@ -81,3 +81,32 @@ def test_invalid_arguments():
     with pytest.raises(_lib.BtcMinerError):
         _lib.split_range(0, 10, 0)
     assert _lib.split_range(10, 5, 3, [1, 2, 3]) == [None, None, None]  # empty range
+
+
+def test_calibrated_rates_ignore_one_outlier_step():
+    """rank-mode calibration takes each rank's median over its
+    warmup steps after the first, and holds a rank at 0.85 of the fastest
+    unless two of its steps agree it is slower.  One injected outlier step
+    (a clock ramp, a late code-object load) leaves the shares within 2% of the
+    steady rates; a rank that is persistently 20% slower keeps its rate."""
+    from distributed_bitcoin_minter_amd.dist import calibrated_rates, shares_from_rates
+    steady = [54.0, 53.2, 55.1, 54.6]
+    steps = [[r * (1 + 0.001 * k) for k in range(4)] for r in steady]
+    steps[1][2] = 20.0          # one transient step on rank 1
+    steps[3][0] = 90.0          # one absurdly fast step on rank 3
+    rates, info = calibrated_rates(steps)
+    want = shares_from_rates(steady)
+    got = shares_from_rates(rates)
+    assert all(abs(g - w) <= 0.02 * w for g, w in zip(got, want)), (got, want)
+    assert info["clamped"] == [] and info["spread"][1] > 0.6 and info["spread"][0] < 0.01
+    # a persistently slow rank: its steps agree, so its rate stands
+    slow = [[43.0, 43.2, 43.1], [54.0, 54.1, 53.9]]
+    rates, info = calibrated_rates(slow)
+    assert info["clamped"] == [] and abs(rates[0] - 43.1) < 1e-9
+    # a rank low in two steps that disagree (46 vs 30): held at 0.85 of the fastest
+    rates, info = calibrated_rates([[46.0, 30.0], [54.0, 54.0]])
+    assert info["clamped"] == [0] and abs(rates[0] - 0.85 * 54.0) < 1e-9
+    # one step per rank (warmup 2): the median is that step; a single low
+    # step cannot agree with another, so below 0.85 of the fastest it is held
+    assert calibrated_rates([[50.0], [54.0]])[0] == [50.0, 54.0]
+    assert calibrated_rates([[40.0], [54.0]])[0] == [0.85 * 54.0, 54.0]

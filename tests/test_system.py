@@ -57,10 +57,12 @@ class OracleSearcher:
 
 
 class System:
-    def __init__(self, chunk, p):
+    def __init__(self, chunk, p, target_ms=0):
+        """target_ms = 0: fixed chunks (these tests pin the tiling); the
+        rate-sized chunks of the product default are tested below."""
         self.p = p
         self.srv = lsp.NewServer(0, p)
-        self.bs = BitcoinServer(self.srv, chunk=chunk)
+        self.bs = BitcoinServer(self.srv, chunk=chunk, target_ms=target_ms)
         self.hostport = f"127.0.0.1:{self.srv.port}"
         self.threads = [threading.Thread(target=self.bs.serve, daemon=True)]
         self.threads[0].start()
@@ -112,7 +114,7 @@ def test_c5_shape_16_clients_4_miners_10pct_drop(oracle):
     10% read and write drop on every endpoint; every client gets the exact
     sequential-scan answer and the load is spread over all miners."""
     p = params(ms=20, k=200)
-    s = System(chunk=600, p=p)
+    s = System(chunk=600, p=p, target_ms=300)  # the product's rate-sized chunks
     searchers = [OracleSearcher(oracle) for _ in range(4)]
     for m in searchers:
         s.add_miner(m)
@@ -251,9 +253,10 @@ class FakeLSP:
         return [(m.Hash, m.Nonce) for c, m in self.sent if c == cid and m.Type == MsgType.Result]
 
 
-def make(chunk, depth=1):
+def make(chunk, depth=1, **kw):
     f = FakeLSP()
-    return f, BitcoinServer(f, chunk=chunk, depth=depth)
+    kw.setdefault("target_ms", 0)  # fixed chunks unless a test asks for rate-sized ones
+    return f, BitcoinServer(f, chunk=chunk, depth=depth, **kw)
 
 
 def test_chunks_tile_the_range_exactly():
@@ -354,8 +357,9 @@ def test_lost_client_results_ignored():
     assert len(f.jobs_for(1)) == 1
 
 
+@pytest.mark.parametrize("target_ms", [0, 300])
 @pytest.mark.parametrize("seed", range(12))
-def test_scheduler_random_event_sequences(seed):
+def test_scheduler_random_event_sequences(seed, target_ms):
     """Random joins, losses, requests, client deaths and out-of-order
     results against the scheduler (no network).  Invariants: every request
     whose client survives is answered exactly once, in its client's order,
@@ -372,7 +376,13 @@ def test_scheduler_random_event_sequences(seed):
     def brute(data, lo, hi):
         return min(((toy_hash(data, n), n) for n in range(lo, hi + 1)), default=(U64, U64))
 
-    f, s = make(rng.choice([1, 3, 7, 50]), depth=rng.choice([1, 2, 3]))
+    now = [0.0]  # a fake clock: rate-sized chunks (target_ms > 0) see random job times
+
+    def clock():
+        now[0] += rng.random() * 0.2
+        return now[0]
+    f, s = make(rng.choice([1, 3, 7, 50]), depth=rng.choice([1, 2, 3]), target_ms=target_ms, clock=clock,
+                max_mult=8)
     next_id = [1]
     miners, clients = set(), {}
     expected = {}  # client -> [answers in order]
@@ -384,7 +394,7 @@ def test_scheduler_random_event_sequences(seed):
     def deliver(mid):
         jobs = s.miners.get(mid)
         if jobs:
-            rid, lo, hi = jobs[0]
+            rid, lo, hi = jobs[0][:3]
             data = next((r.data for r in s.requests.values() if r.rid == rid), "gone")
             s._on_message(mid, NewResult(*brute(data, lo, hi)))
 
@@ -468,4 +478,109 @@ def test_server_survives_malformed_client_payloads(oracle):
     got = Message.unmarshal(c.Read())
     assert (got.Type, got.Hash, got.Nonce) == (MsgType.Result, 1419516646206828, 9898)
     c.Close()
+    s.close()
+
+
+# ---- rate-sized chunks (round 6) --------------------------
+
+def test_chunk_for_policy():
+    """server.chunk_for: about target_s of the miner's work, rounded to whole
+    base chunks, in [1, max_mult], at most twice the previous multiple, at
+    most the miner's rate share of what the request has left."""
+    from distributed_bitcoin_minter_amd.server import chunk_for
+    B = 1 << 32
+    assert chunk_for(B, 0.3, 64, None, 0, 1 << 40, 0.5) == 1              # no rate yet: one base
+    assert chunk_for(B, 0.0, 64, 1e12, 8, 1 << 40, 0.5) == 1              # sizing off
+    assert chunk_for(B, 0.3, 64, 55e9, 4, 1 << 40, 0.5) == 4              # 16.5 G = 3.8 bases
+    assert chunk_for(B, 0.3, 64, 440e9, 4, 1 << 50, 0.9) == 8             # 31 bases, ramp: 2 x 4
+    assert chunk_for(B, 0.3, 64, 440e9, 32, 1 << 50, 0.9) == 31
+    assert chunk_for(B, 0.3, 16, 440e9, 32, 1 << 50, 0.9) == 16           # cap
+    assert chunk_for(B, 0.3, 64, 440e9, 32, 10 * B, 0.5) == 5             # its share of the tail
+    assert chunk_for(B, 0.3, 64, 1e3, 1, 1 << 40, 0.01) == 1              # never below one base
+
+
+def _simulate(rates, base, target_ms, nonces, depth=2, max_mult=64):
+    """The scheduler against miners of given rates (nonces/s) on a simulated
+    clock: each miner works through its jobs in order and answers each one
+    when its nonces are done.  Returns (per miner: the sizes of its jobs,
+    the simulated seconds)."""
+    import heapq
+    now = [0.0]
+    f, s = make(base, depth=depth, target_ms=target_ms, max_mult=max_mult, clock=lambda: now[0])
+    mids = list(range(1, len(rates) + 1))
+    for m in mids:
+        s._on_message(m, NewJoin())
+    s._on_message(100, NewRequest("x", 0, nonces - 1))
+    busy_until = {m: 0.0 for m in mids}
+    done = {m: 0 for m in mids}
+    events = []
+
+    def plan(m):  # queue the completion of m's next unplanned job
+        jobs = f.jobs_for(m)
+        while done[m] < len(jobs) and len([e for e in events if e[1] == m]) < 1:
+            lo, hi = jobs[done[m]]
+            t = max(now[0], busy_until[m]) + (hi - lo + 1) / rates[m - 1]
+            busy_until[m] = t
+            heapq.heappush(events, (t, m, lo, hi))
+            break
+    for m in mids:
+        plan(m)
+    while events:
+        t, m, lo, hi = heapq.heappop(events)
+        now[0] = t
+        done[m] += 1
+        s._on_message(m, NewResult(lo, lo))
+        for x in mids:
+            plan(x)
+    assert f.results_for(100) == [(0, 0)]
+    return {m: [b - a + 1 for a, b in f.jobs_for(m)] for m in mids}, now[0]
+
+
+def test_fast_miner_gets_proportionally_larger_chunks():
+    """Two miners, one 8x faster: once the rates are measured, the fast one's
+    jobs are about 8x the slow one's (each about target_ms of its own work),
+    and the request's tail is split by rate so both finish close together.
+    With fixed chunks the same run takes far more jobs."""
+    base = 1000
+    rates = [160_000.0, 20_000.0]           # nonces/s: 8x apart
+    sizes, secs = _simulate(rates, base, 200, 4_000_000)
+    fast, slow = sizes[1], sizes[2]
+    # steady state: the middle of the run (ramp-up before, the tail after)
+    f_mid = sorted(fast)[len(fast) // 2]
+    s_mid = sorted(slow)[len(slow) // 2]
+    assert f_mid == 32 * base and s_mid == 4 * base, (fast, slow)   # 0.2 s of each miner's work
+    assert 7.0 <= f_mid / s_mid <= 9.0
+    ideal = 4_000_000 / sum(rates)
+    assert secs < ideal * 1.15, (secs, ideal)
+    fixed, secs_fixed = _simulate(rates, base, 0, 4_000_000)
+    assert len(fixed[1]) + len(fixed[2]) == 4000 and len(fast) + len(slow) < 300
+    # the wire format is unchanged: every job is an inclusive [Lower, Upper]
+    # tile of the request, in base multiples except the request's end
+
+
+def test_rate_sized_chunks_end_to_end(oracle):
+    """The same over the network: two CPU miners whose searches take time in
+    proportion to their nonces, one 8x faster; the answer is the sequential
+    scan's and the fast miner's median job is about 8x the slow one's."""
+    class Paced(OracleSearcher):
+        def __init__(self, oracle, rate):
+            super().__init__(oracle)
+            self.rate = rate
+
+        def search(self, data, lo, hi):
+            self.jobs.append((lo, hi))
+            time.sleep((hi - lo + 1) / self.rate)
+            return self.oracle.search(data.encode(), lo, hi)
+
+    p = params(ms=20, k=100)
+    s = System(chunk=2000, p=p, target_ms=200)
+    fast, slow = Paced(oracle, 400_000), Paced(oracle, 50_000)
+    s.add_miner(fast)
+    s.add_miner(slow)
+    s.wait(lambda: s.bs.stats["joins"] == 2)
+    n = 1_200_000
+    assert client.request(s.hostport, "paced", n - 1, p) == oracle.search(b"paced", 0, n - 1)
+    med = lambda js: sorted(b - a + 1 for a, b in js)[len(js) // 2]  # noqa: E731
+    ratio = med(fast.jobs) / med(slow.jobs)
+    assert 4.0 <= ratio <= 12.0, (fast.jobs, slow.jobs)
     s.close()

@@ -26,10 +26,13 @@
 #   ab_padk     the same for search_kernel_padk<P, 1> (L = 109..117) and <P, 2> (L = 173..181)
 #   parity_pad  the padding-block parity tests and every kernel layout
 #   ab          A/B of library variants: AB_LIBS="a.so b.so" (parity of each first, then alternating)
-# Logs and profiles land in gpurun_out/$TAG (TAG defaults to r05).
+#   callsize    tools/call_size.py: GH/s of whole calls of 2^24 .. 2^34 nonces, one device and 8 slots on GPU 0
+#   pmc_c2      the C2 PMC passes only (with each kernel's code hash in the summary, tools/pmc_summary.py)
+#   rehearse_one  2 torchrun ranks on GPU 0 (--rehearse-one-gpu) with the C4 step and the one-process C4 block
+# Logs and profiles land in gpurun_out/$TAG (TAG defaults to r06).
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 step() {  # name, seconds, command...
@@ -101,6 +104,20 @@ for phase in "$@"; do
           SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE \
           -d "$OUT/pmc_${C}_sq" -o s --output-format csv -- python3 tools/prof_one.py $C 2
       done ;;
+    callsize) step call_size 300 python -u tools/call_size.py --out "$OUT/call_size.json" ;;
+    pmc_c2)
+      C=C2
+      step pmc_${C}_fetch 90 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_${C}_fetch" -o f --output-format csv \
+        -- python3 tools/prof_one.py $C 2
+      step pmc_${C}_write 90 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_${C}_write" -o w --output-format csv \
+        -- python3 tools/prof_one.py $C 2
+      step pmc_${C}_sq 90 env PROF_ONE_LAUNCHES="$OUT/pmc_${C}_launches.json" rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU \
+        SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE \
+        -d "$OUT/pmc_${C}_sq" -o s --output-format csv -- python3 tools/prof_one.py $C 2
+      step pmc_summary 60 python3 tools/pmc_summary.py "$OUT" "$OUT" C2 ;;
+    rehearse_one)
+      step rehearse2_c4_one 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 2 --steps 2 --warmup 2 --rehearse-one-gpu ;;
     parity) step parity_campaign 600 python -u tools/parity_campaign.py ${PARITY_CASES:-3000} ${PARITY_SEED:-303} ;;
     lensweep) step len_sweep 600 python -u tools/len_sweep.py --max-len 130 ;;
     lensweep_pmc)

@@ -10,13 +10,22 @@ are read and the summary is written as pmc_summary_<config>.json (what
 bench.py looks up for that config's roofline fields).  With the call's
 launches (<gpurun_out>/pmc_<config>_launches.json, written by
 tools/prof_one.py under PROF_ONE_LAUNCHES) each kernel also gets
-valu_per_nonce = SQ_INSTS_VALU x 64 / the nonces of its main launch."""
+valu_per_nonce = SQ_INSTS_VALU x 64 / the nonces of its main launch.
+Each kernel also gets code_sha: the sha256 of its instruction bytes in the
+library the passes ran (BTCMINER_LIB, else the in-tree libbtcminer.so;
+distributed_bitcoin_minter_amd/codeobj.py), so that bench.py can tell whether
+an imported summary describes the kernel it loaded (roofline.pmc.same_kernel)."""
 import collections
 import csv
 import glob
 import json
 import os
+import re
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from distributed_bitcoin_minter_amd import codeobj  # noqa: E402
 
 out_dir = sys.argv[1]
 src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out"
@@ -64,6 +73,16 @@ for k, disp in per.items():
         if name + "(" in k and "SQ_INSTS_VALU" in m:
             e["nonces_per_launch"] = nn
             e["valu_per_nonce"] = m["SQ_INSTS_VALU"] * 64 / nn
+    lib = os.environ.get("BTCMINER_LIB") or os.path.join(ROOT, "distributed_bitcoin_minter_amd", "libbtcminer.so")
+    mk = re.search(r"search_kernel(_padc|_padk)?<(\d+), (\d+)(?:, (\d+))?>", k)
+    if mk:
+        p, a = int(mk.group(2)), int(mk.group(3))
+        kind = mk.group(1)
+        nbv, pad = (1, 2) if kind == "_padc" else (1, 2 + a) if kind == "_padk" else (a, 0)
+        sha = codeobj.kernel_code_sha(lib, p, nbv, pad)
+        if sha:
+            e["code_sha"] = sha
+            e["code_lib"] = os.path.relpath(lib, ROOT)
     if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
         e["hbm_bytes_per_launch"] = int((m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024)
     if "GRBM_GUI_ACTIVE" in m and m["_dur_s"] >= MIN_CLOCK_S:
