@@ -217,20 +217,21 @@ int blocks_per_cu(bm_ctx* ctx, DeviceCtx& d, const void* fn) {
 // Returns K, or -1 when the generic kernel must run.
 int pad_fold_k(const bm_segment_t& s) {
     if (!s.pad_block || s.nbv != 1 || s.p < 55) return -1;
+    // the only K this padding block can be: its bit length 8 * (64K + P + 1)
+    const uint32_t bits = s.pad_w[15];
+    if (bits % 8 != 0 || bits / 8 < (uint32_t)s.p + 1 || (bits / 8 - s.p - 1) % 64 != 0) return -1;
+    const uint32_t k = (bits / 8 - s.p - 1) / 64;
+    if (k > (uint32_t)kMaxPadPrefixBlocks) return -1;
     uint32_t w[64];
     for (int i = 0; i < 16; ++i) w[i] = s.pad_w[i];
     host::expand(w);
-    for (int k = 0; k <= kMaxPadPrefixBlocks; ++k) {
-        const KW64 kw = pad_kw_const(s.p, k);
-        bool same = true;
-        for (int t = 0; t < 64 && same; ++t) same = kK256[t] + w[t] == kw.v[t];
-        if (!same) continue;
-        if (k == 0)
-            for (int q = 0; q < 8; ++q)
-                if (s.mid[q] != kIV256[q]) return -1;
-        return k;
-    }
-    return -1;
+    const KW64 kw = pad_kw_const(s.p, (int)k);
+    for (int t = 0; t < 64; ++t)
+        if (kK256[t] + w[t] != kw.v[t]) return -1;
+    if (k == 0)
+        for (int q = 0; q < 8; ++q)
+            if (s.mid[q] != kIV256[q]) return -1;
+    return (int)k;
 }
 
 int size_launch(bm_ctx* ctx, DeviceCtx& d, const bm_segment_t& s, uint32_t part_off, Launch& L) {

@@ -339,7 +339,11 @@ BM_DEV uint64_t readfirstlane_u64(uint64_t v) {
 #endif
 // NBV = 2 layouts whose inner loop spills at 7 waves/SIMD (72 VGPRs) keep 6
 // (tools/check_inner.py: 0 layouts with scratch in the inner loop).
-constexpr bool nbv2_tight(int P) { return P == 4 || P == 13 || P == 14; }
+// BM_NBV2_TIGHT=0 gives them 7 too (an A/B knob, round 6).
+#ifndef BM_NBV2_TIGHT
+#define BM_NBV2_TIGHT 1
+#endif
+constexpr bool nbv2_tight(int P) { return BM_NBV2_TIGHT && (P == 4 || P == 13 || P == 14); }
 constexpr int search_waves(int P, int NBV) {
     return (NBV == 1 && P >= 55) ? BM_WAVES_PAD
                                  : (NBV == 2 ? (nbv2_tight(P) ? 6 : BM_WAVES_NBV2) : BM_WAVES_MAIN);

@@ -34,7 +34,7 @@ constexpr uint32_t kIV256[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53
 // message length in bits, 8 * (64K + P + 1), W1..W14 = 0, W16..W63 expanded
 // at compile time.  The folded padding-block kernels (bm_kernels.hpp:
 // search_kernel_padc, K = 0, whose entering state is the IV; search_kernel_padk,
-// K = 1 or 2, after a midstate) use these as literal operands instead of 64
+// K = 1..kMaxPadPrefixBlocks, after a midstate) use these as literal operands instead of 64
 // kernarg SGPRs; the launcher checks a segment against them at run time.
 struct KW64 {
     uint32_t v[64];
@@ -55,7 +55,11 @@ constexpr KW64 pad_kw_const(int P, int K = 0) {
 }
 template <int P, int K = 0>
 inline constexpr KW64 kPadKW = pad_kw_const(P, K);
-constexpr int kMaxPadPrefixBlocks = 2;  // search_kernel_padk<P, K>: K = 1..2 prefix blocks
+// search_kernel_padk<P, K>: K = 1..15 prefix blocks, i.e. "msg nonce" up to
+// 64 * 15 + 64 = 1,024 bytes -- every message an LSP packet can carry (about
+// 1,000 bytes, README:61; the reference's readers take 1,500-byte datagrams,
+// lsp/client_impl.go:172).  Longer messages run the generic kernel.
+constexpr int kMaxPadPrefixBlocks = 15;
 
 namespace host {
 

@@ -14,6 +14,9 @@ Messages are L bytes 'a'.. (tools/len_sweep.py's); lengths:
   114 byte 60 of block 1: padding block after a prefix block (the generic kernel
       until round 4; search_kernel_padk<60, 1> since round 5)
   178 byte 60 of block 2: padding block after two prefix blocks, search_kernel_padk<60, 2>
+  242 byte 60 of block 3: after three prefix blocks, search_kernel_padk<60, 3> (round 6)
+  1010 byte 60 of block 15: after fifteen, search_kernel_padk<60, 15> (round 6: the
+      largest folded K, a message of about an LSP packet's 1,000 bytes)
   59  digits straddle blocks 0 and 1: NBV = 2
 
 Usage: python tests/golden/make_layout_golden.py [--threads T] [--lengths 178 ...]
@@ -30,7 +33,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 CLI = os.path.join(ROOT, "oracle", "oracle_cli")
 LENGTHS = {50: "padc", 46: "padc, two-word inner loop", 114: "padding block after one prefix block",
-           59: "NBV = 2", 178: "padding block after two prefix blocks"}
+           59: "NBV = 2", 178: "padding block after two prefix blocks",
+           242: "padding block after three prefix blocks", 1010: "padding block after fifteen prefix blocks"}
 LO = 10 ** 9
 HI = LO + (1 << 32) - 1
 

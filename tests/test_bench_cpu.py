@@ -324,10 +324,14 @@ def test_kernel_names_and_isa_keys():
     assert bench.kernel_name(60, 1, 4) == "search_kernel_padk<60, 2, 1>" and bench.isa_key(60, 1, 4) == "60:k2"
     lay = json.load(open(os.path.join(ROOT, "distributed_bitcoin_minter_amd", "csrc", "isa_mix.json")))["layouts"]
     for p in range(55, 64):
-        for k in (1, 2):
+        for k in range(1, 16):  # round 6: K = 3..15 too (messages up to 1,024 bytes)
             assert lay[f"{p}:k{k}"]["issue_slots"] <= lay[f"{p}:1"]["issue_slots"], (p, k)
             assert lay[f"{p}:k{k}"]["readlanes"] == 0, (p, k)  # no spilled SGPR read back per nonce
-    assert lay["56:1"]["readlanes"] == 24  # the generic kernel's (messages with >= 3 prefix blocks)
+    assert lay["56:1"]["readlanes"] == 24  # the generic kernel's (messages with >= 16 prefix blocks)
+    # round 6: the NBV = 2 inner loops read no spilled SGPR back (isa_mix's old
+    # pick, the per-task block, showed 21 and 17 for these two)
+    assert lay["13:2"]["readlanes"] == 0 and lay["14:2"]["readlanes"] == 0
+    assert bench.kernel_name(60, 1, 17) == "search_kernel_padk<60, 15, 1>" and bench.isa_key(60, 1, 17) == "60:k15"
     assert bench.issue_bound("60:k1", 2.4)["GHs_per_gpu"] > bench.issue_bound("60:1", 2.4)["GHs_per_gpu"]
 
 

@@ -152,15 +152,16 @@ def test_padding_block_layouts_folded_and_generic(gpu_ctx, generic_pad_ctx, orac
     SHA-256's length words spill into a block of their own), 10-digit
     nonces, both task shapes: a message of K whole prefix blocks plus the
     varying one runs the kernel with the padding block's constants folded --
-    K = 0: search_kernel_padc (IV folded too; stats pad_block = 2), K = 1, 2:
-    search_kernel_padk<P, K> (midstate from kernargs; pad_block = 3, 4,
-    VERDICT r4) -- and K = 3, or any K under BTCMINER_PADC=0, the generic
+    K = 0: search_kernel_padc (IV folded too; stats pad_block = 2), K = 1..15:
+    search_kernel_padk<P, K> (midstate from kernargs; pad_block = 2 + K;
+    K = 1, 2 since round 5, 3..15 since round 6: every message an LSP packet
+    carries) -- and K = 16, or any K under BTCMINER_PADC=0, the generic
     kernel (pad_block = 1); every answer equals the oracle's."""
     lo = 10 ** 9 + 7_777_777
     hi = lo + 20_000
-    msgs = [bytes(97 + (i + k) % 26 for i in range(P - 10 + 64 * k)) for k in range(4)]  # ends at byte P of block k
-    runs = [(gpu_ctx, msgs[k], 2 + k) for k in range(3)] + [(gpu_ctx, msgs[3], 1)]
-    runs += [(generic_pad_ctx, msgs[k], 1) for k in range(3)]
+    msgs = [bytes(97 + (i + k) % 26 for i in range(P - 10 + 64 * k)) for k in range(17)]  # ends at byte P of block k
+    runs = [(gpu_ctx, msgs[k], 2 + k) for k in range(16)] + [(gpu_ctx, msgs[16], 1)]
+    runs += [(generic_pad_ctx, msgs[k], 1) for k in (0, 1, 2, 3, 15)]
     for ctx, msg, pad in runs:
         want = oracle.search(msg, lo, hi, threads=8)
         for td in (0, 2):
@@ -192,7 +193,8 @@ def test_layout_full_range_goldens(gpu_ctx, case):
     assert gpu_ctx.search(msg, case["lower"], case["upper"]) == (case["hash"], case["nonce"])
     st = gpu_ctx.last_stats()
     dom = max((st.launch[i] for i in range(st.recorded)), key=lambda x: x.nonces)
-    want = {50: (1, 2), 46: (1, 2), 114: (1, 3), 59: (2, 0), 178: (1, 4)}[case["len"]]  # 114, 178: padk<P, K>
+    # 114, 178, 242, 1010: padk<60, K> with K = 1, 2, 3, 15 (pad_block 2 + K)
+    want = {50: (1, 2), 46: (1, 2), 114: (1, 3), 59: (2, 0), 178: (1, 4), 242: (1, 5), 1010: (1, 17)}[case["len"]]
     assert (dom.nbv, dom.pad_block) == want, (dom.nbv, dom.pad_block)
 
 

@@ -7,6 +7,11 @@ per length the dominant launch's rate per build and its ratio to the
 product's, checks the answers agree, and a mean ratio per build.
 
     AB_LIBS="v1=a.so v2=b.so" python tools/ab_lens.py 55-60,8 [reps] [nonces]
+
+AB_LO sets the range's start (default 10^9), AB_MAXWIN the planner's window
+cap (bm_ctx_set_max_windows; 0 makes every range whose high digits sit in an
+earlier block an NBV = 2 launch): e.g. AB_LO=10^15 AB_MAXWIN=0 with L = 61, 62
+reaches <13, 2>, <14, 2> (16-digit nonces, 2 and 1 digits in the block before).
 """
 import json
 import os
@@ -29,13 +34,15 @@ def main():
     lens = lengths(sys.argv[1] if len(sys.argv) > 1 else "55-60,8")
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 31
-    lo = 10 ** 9
+    lo = int(os.environ.get("AB_LO", 10 ** 9))
     ctxs = [("product", Context(devices=[0]))]
     for spec in os.environ.get("AB_LIBS", "").split():
         name, path = spec.split("=", 1)
         ctxs.append((name, Context(devices=[0], lib_path=os.path.abspath(path))))
     for _, c in ctxs:
         c.set_timing(True)
+        if os.environ.get("AB_MAXWIN"):
+            c.set_max_windows(int(os.environ["AB_MAXWIN"]))
     ratios = {name: [] for name, _ in ctxs[1:]}
     for L in lens:
         msg = bytes(97 + (i % 26) for i in range(L))

@@ -24,6 +24,7 @@
 #               (every layout a 10-digit search hits); lensweep_pmc: its SQ_INSTS_VALU pass
 #   ab_padc     A/B of search_kernel_padc against the generic padding-block kernel (L = 45..53)
 #   ab_padk     the same for search_kernel_padk<P, 1> (L = 109..117) and <P, 2> (L = 173..181)
+#   ab_padk3    the same for <P, 3> (L = 237..245) and <P, 15> (L = 1005..1013), round 6
 #   parity_pad  the padding-block parity tests and every kernel layout
 #   ab          A/B of library variants: AB_LIBS="a.so b.so" (parity of each first, then alternating)
 #   callsize    tools/call_size.py: GH/s of whole calls of 2^24 .. 2^34 nonces, one device and 8 slots on GPU 0
@@ -104,6 +105,10 @@ for phase in "$@"; do
           SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE \
           -d "$OUT/pmc_${C}_sq" -o s --output-format csv -- python3 tools/prof_one.py $C 2
       done ;;
+    ab_nbv2_tight)
+      # <4, 2>, <12, 2> (control), <13, 2>, <14, 2> at 7 waves (BM_NBV2_TIGHT=0 build) against the product's 6
+      step ab_nbv2_tight 300 env AB_LO=1000000000000000 AB_MAXWIN=0 \
+        AB_LIBS="t7=$D/libbtcminer_t7.so" python -u tools/ab_lens.py 52,60-62 5 2147483648 ;;
     callsize) step call_size 300 python -u tools/call_size.py --out "$OUT/call_size.json" ;;
     pmc_c2)
       C=C2
@@ -129,6 +134,10 @@ for phase in "$@"; do
     ab_padk)
       step ab_padk1 300 env AB_LENS=109-117 python -u tools/ab_padc.py ${AB_REPS:-5}
       step ab_padk2 300 env AB_LENS=173-181 python -u tools/ab_padc.py ${AB_REPS:-5} ;;
+    ab_padk3)
+      # round 6: search_kernel_padk<P, 3> (L = 237..245) and <P, 15> (L = 1005..1013) against the generic kernel
+      step ab_padk3 300 env AB_LENS=237-245 python -u tools/ab_padc.py ${AB_REPS:-5}
+      step ab_padk15 300 env AB_LENS=1005-1013 python -u tools/ab_padc.py ${AB_REPS:-5} ;;
     structure)
       # C2's 11 launches against one 10-digit range of the same size, live clock
       step structure 300 python -u tools/ab_structure.py 8
