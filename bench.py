@@ -794,7 +794,7 @@ def _c4_one_process_child(args, n):
     lines = [ln for ln in out.strip().splitlines() if ln.startswith("{")]
     if p.returncode != 0 or not lines:
         return {"skipped": f"the one-process child exited {p.returncode}", "stderr_tail": err[-800:]}
-    return one_process_block(json.loads(lines[-1]), n, wall, cmd[2:])
+    return one_process_block(json.loads(lines[-1]), n, wall, ["bench.py"] + cmd[3:])
 
 
 def child_env(environ):

@@ -274,7 +274,8 @@ def test_bench_torchrun_rehearsal_c4_one_process():
     assert one["combine"] == "host" and one["scaling_valid"] is False and one["GHs"] > 10, one
     assert len(one["devices"]) == 2 and sum(d["nonces"] for d in one["devices"]) == 2 ** 40, one
     assert all("start_ms" in d and "allgather_ms" in d for d in one["devices"]) and one["start_threads"] == 2
-    assert "bm_ctx_create(2)" in one["design"] and "--rehearse-one-gpu" in one["child_cmd"]
+    assert "bm_ctx_create(2)" in one["design"] and one["child_cmd"].startswith("bench.py --gpus 2 --config C4")
+    assert "--rehearse-one-gpu" in one["child_cmd"]
 
 
 def test_bench_torchrun_rccl_world1():
@@ -293,6 +294,10 @@ def test_bench_torchrun_rccl_world1():
     assert pm["imported"] is True and pm["src"].startswith("profiles/") and pm["box_clock_ghz"] > 1.0, pm
     assert pm["valu_per_nonce"] > 1000 and 0.3 < pm["valu_dual_issued_frac"] < 0.6, pm  # C2: 0.477
     assert roof["traffic"] == pm["hbm_bytes_per_launch"] and roof["traffic_imported"] is True
+    # the imported pass is tied to the kernel this run loaded (the
+    # sha256 of its instructions in the library's gfx950 code object)
+    assert pm["src"].startswith("profiles/r06/") and pm["same_kernel"] is True, pm
+    assert pm["code_sha"] == pm["loaded_code_sha"] and len(pm["code_sha"]) == 64
     for k in ("valu_per_nonce_pmc", "valu_dual_issued_frac_pmc", "clock_ghz_pmc"):
         assert k not in roof, k
     assert "imported" in roof["executed"]["src"], roof["executed"]

@@ -89,14 +89,17 @@ def test_c5_gpu_miners_16_clients_10pct_drop(gpu_ctx, oracle):
         assert got.get(i) == gpu_ctx.search(msgs[i].encode(), 0, tops[i]), i
     for i in (0, 15):
         assert got[i] == oracle.search(msgs[i].encode(), 0, tops[i], threads=8), i
-    assert bs.stats["chunks_done"] >= 16 * 16
+    # jobs are multiples of the 2^24 base sized by each miner's rate (round 6):
+    # every request still went out in several chunks, and every nonce was sent
+    assert bs.stats["chunks_done"] >= 16 * 2 and bs.stats["nonces_sent"] >= sum(t + 1 for t in tops)
     stop(bs, threads, gm)
 
 
 @pytest.mark.parametrize("cfg", ["C5"])
 def test_c5_at_size_against_cpu_goldens(cfg):
     """BASELINE C5 at its full size: 16 clients, each asking for [0, 2^34-1]
-    of "client-%02d", 2^32-nonce jobs (the server default), 4 GPU miners
+    of "client-%02d", jobs of 2^32-nonce multiples sized by each miner's rate
+    (the server default since round 6: about 300 ms each), 4 GPU miners
     sharing the box's GPU, 10% read and write drop at every endpoint.
     Every answer equals a full CPU scan of that client's 2^34 nonces
     (tests/golden/c5_clients.json, AVX-512 oracle)."""
@@ -128,7 +131,7 @@ def test_c5_at_size_against_cpu_goldens(cfg):
     lspnet.ResetDropPercent()
     for i, m in enumerate(msgs):
         assert got.get(i) == tuple(gold["clients"][m]), (m, got.get(i))
-    assert bs.stats["chunks_done"] >= 16 * 4
+    assert bs.stats["chunks_done"] >= 16 * 2 and bs.stats["nonces_sent"] >= 16 << 34
     print(f"C5 at size: {16 << 34} nonces in {secs:.2f} s = {(16 << 34) / secs / 1e9:.2f} GH/s end to end")
     stop(bs, threads, gm)
 
