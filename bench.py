@@ -738,7 +738,10 @@ def c4_block(args, ctx, grp, search, n):
     return out
 
 
-ONE_PROCESS_TIMEOUT_S = 300  # the one-process C4 child: set-up, warm-up and timed steps over N devices
+# the one-process C4 child: set-up, warm-up and timed steps over N devices
+# (N = 2: about 35 s; a one-GPU rehearsal at N = 8: about 25 s); a child that
+# hangs costs the line at most this much
+ONE_PROCESS_TIMEOUT_S = 180
 
 
 def c4_one_process(args, grp, n):

@@ -337,13 +337,17 @@ BM_DEV uint64_t readfirstlane_u64(uint64_t v) {
 #ifndef BM_WAVES_NBV2
 #define BM_WAVES_NBV2 7
 #endif
-// NBV = 2 layouts whose inner loop spills at 7 waves/SIMD (72 VGPRs) keep 6
-// (tools/check_inner.py: 0 layouts with scratch in the inner loop).
-// BM_NBV2_TIGHT=0 gives them 7 too (an A/B knob, round 6).
+// NBV = 2 layouts kept at 6 waves/SIMD.  Until round 6 that was P = 4, 13
+// and 14, whose inner loops spilled at 7 (72 VGPRs).  Round 6: at 7, P = 13
+// and 14 compile with no scratch, readlane or memory op in the inner loop
+// (tools/check_inner.py), and measured +0.25% / +0.57% against 6 (-0.3% on
+// an unchanged control layout; profiles/r06/ab_nbv2_tight.log), so they run
+// at 7 now; P = 4 measured -0.8% at 7 and keeps 6.  BM_NBV2_TIGHT=0 gives
+// P = 4 7 too (the A/B knob).
 #ifndef BM_NBV2_TIGHT
 #define BM_NBV2_TIGHT 1
 #endif
-constexpr bool nbv2_tight(int P) { return BM_NBV2_TIGHT && (P == 4 || P == 13 || P == 14); }
+constexpr bool nbv2_tight(int P) { return BM_NBV2_TIGHT && P == 4; }
 constexpr int search_waves(int P, int NBV) {
     return (NBV == 1 && P >= 55) ? BM_WAVES_PAD
                                  : (NBV == 2 ? (nbv2_tight(P) ? 6 : BM_WAVES_NBV2) : BM_WAVES_MAIN);
