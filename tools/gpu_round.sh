@@ -59,6 +59,7 @@ for phase in "$@"; do
     smoke) step smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step gpu_tests 1200 $PYTEST tests -m gpu -v ;;
     tests_multi) step gpu_tests_multi 600 $PYTEST tests/test_gpu_multi.py -m gpu -v ;;
+    tests_k) step gpu_tests_k 600 $PYTEST tests -m gpu -v -k "${TESTS_K}" ;;
     bench) step bench_C2 300 python -u bench.py --steps 20 --warmup 5 ;;
     bench_c3) step bench_C3 300 $BENCH --config C3 --steps 20 --warmup 5 ;;
     bench_c4) step bench_C4 300 $BENCH --config C4 --steps 2 --warmup 1 ;;
