@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <condition_variable>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -144,6 +145,85 @@ void trace(const char* fmt, ...) {
         if (e_ != hipSuccess) return hip_status(e_); \
     } while (0)
 
+// The submission threads of a multi-device context: created once,
+// at the context's first search over several devices, and kept until the
+// context is destroyed, so a search does not create and join N - 1 threads
+// (about 0.2 ms at N = 8, most of a small job's fixed cost).
+// run(n, f) runs f(1) .. f(n - 1) on the pool's threads and f(0) on the
+// caller, and returns when all of them have.  f must not throw (the search
+// wraps it in guarded()).  A context is not re-entrant, so one run at a time.
+class SubmitPool {
+   public:
+    SubmitPool() = default;
+    SubmitPool(const SubmitPool&) = delete;
+    SubmitPool& operator=(const SubmitPool&) = delete;
+    ~SubmitPool() { stop(); }
+
+    // false when the threads could not be started: the caller submits serially
+    bool run(int n, const std::function<void(int)>& f) {
+        if (!ensure(n - 1)) return false;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &f;
+            pending_ = n - 1;
+            ++gen_;
+        }
+        work_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [&] { return pending_ == 0; });
+        job_ = nullptr;
+        return true;
+    }
+    int threads() const { return (int)th_.size(); }
+
+   private:
+    bool ensure(int k) {
+        if ((int)th_.size() == k) return true;
+        stop();  // (a context's device count never changes; this is only the first call)
+        try {
+            for (int i = 0; i < k; ++i) th_.emplace_back([this, i] { loop(i + 1); });
+        } catch (const std::system_error&) {
+            stop();
+            return false;
+        }
+        return true;
+    }
+    void loop(int di) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* job;
+            {
+                std::unique_lock<std::mutex> l(m_);
+                work_.wait(l, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                job = job_;
+            }
+            (*job)(di);
+            std::lock_guard<std::mutex> g(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    void stop() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            quit_ = true;
+        }
+        work_.notify_all();
+        for (auto& t : th_) t.join();
+        th_.clear();
+        quit_ = false;
+    }
+    std::mutex m_;
+    std::condition_variable work_, done_;
+    std::vector<std::thread> th_;
+    const std::function<void(int)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool quit_ = false;
+};
+
 // Restores the caller's current device on scope exit.
 struct DeviceGuard {
     int prev = -1;
@@ -188,6 +268,8 @@ struct bm_ctx {
     std::shared_ptr<bm::JoinJob> pending_join;
     std::thread pending_worker;
     bm_stats_t stats;
+    bm::SubmitPool submit;  // multi-device: one submission thread per device but the first (last member:
+                            // stopped first, when every device is idle)
 };
 
 extern "C" void bm_register_search_kernel(int p, int nbv, const void* fn) {
@@ -567,10 +649,11 @@ int guarded(F&& f) noexcept {
 }
 
 // Stage 2 of a search: every device's work.  A context of several devices
-// submits each device's work from a host thread of its own, so device N-1
-// does not wait for the other devices' ~15 API calls each before it starts
-// (the start skew of a serial submission; bm_stats_t.dev_start_ms reports
-// what is left of it).
+// submits each device's work from a host thread of its own (the context's
+// SubmitPool, kept across searches since round 6), so device N-1 does not
+// wait for the other devices' ~15 API calls each before it starts (the start
+// skew of a serial submission; bm_stats_t.dev_start_ms reports what is left
+// of it).
 int enqueue(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches, std::vector<uint32_t>& first) {
     const int ndev = (int)ctx->devs.size();
     if (ctx->fault_after == 0) return BM_EINTERNAL;  // test hook (also for a rank with nothing to scan)
@@ -579,18 +662,16 @@ int enqueue(bm_ctx* ctx, std::vector<std::vector<Launch>>& launches, std::vector
     auto one = [&](int di) { return guarded([&] { return enqueue_device(ctx, di, launches[di], first[di], enqueued); }); };
     if (ndev == 1) return one(0);
     std::vector<int> rc(ndev, BM_OK);
-    std::vector<std::thread> th;
-    th.reserve(ndev - 1);
-    for (int di = 1; di < ndev; ++di) {
-        try {
-            th.emplace_back([&, di] { rc[di] = one(di); });
-        } catch (const std::system_error&) {  // no thread: this one submits that device's work itself
-            rc[di] = one(di);
-        }
+    const std::function<void(int)> job = [&](int di) { rc[di] = one(di); };
+    bool pooled = false;
+    try {
+        pooled = ctx->submit.run(ndev, job);
+    } catch (...) {  // std::function or the pool's own bookkeeping: submit serially
+        pooled = false;
     }
-    rc[0] = one(0);
-    for (auto& t : th) t.join();
-    ctx->stats.start_threads = 1 + (int)th.size();
+    if (!pooled)  // no threads: this one submits every device's work itself
+        for (int di = 0; di < ndev; ++di) rc[di] = one(di);
+    ctx->stats.start_threads = pooled ? 1 + ctx->submit.threads() : 1;
     for (int r : rc)
         if (r != BM_OK) return r;
     return BM_OK;

@@ -89,3 +89,27 @@ def test_contexts_on_concurrent_threads():
     assert not any(t.is_alive() for t in ts), "a thread did not finish"
     assert not errs, errs
     assert not bad, bad[:5]
+
+
+def test_multi_slot_context_from_fresh_threads_keeps_its_submission_pool():
+    """Round 6: a multi-device context keeps one submission thread
+    per device but the first across searches (its SubmitPool), whatever OS
+    thread calls it -- cgo moves goroutines between threads.  Twelve searches
+    of a 4-slot context, each from a new thread, then a close: every answer
+    equals the oracle's, every call reports 4 submitting threads, and the
+    close returns (the pool's threads end with the context)."""
+    import threading
+    from distributed_bitcoin_minter_amd import Context
+    cases = [(b"bradfitz", 0, 9999, (1419516646206828, 9898)), (b"msg", 0, 2, (4754799531757243342, 1))]
+    got, threads = [], []
+    with Context(devices=[0, 0, 0, 0]) as c:
+        for i in range(12):
+            msg, lo, hi, want = cases[i % 2]
+
+            def go():
+                got.append((c.search(msg, lo, hi), want, c.last_stats().start_threads))
+            t = threading.Thread(target=go)
+            t.start()
+            t.join(timeout=60)
+            threads.append(t)
+    assert len(got) == 12 and all(g == w and n == 4 for g, w, n in got), got

@@ -12,7 +12,7 @@ times and for at least `--min-s` seconds; the rate is nonces / mean wall time
 per call (host wall clock around the synchronous call).  `eff` is that rate
 over the largest size's on the same context.
 
-    python tools/call_size.py [--slots 8] [--min-bits 24] [--max-bits 34] [--out f.json]
+    python tools/call_size.py [--slots 8] [--min-bits 24] [--max-bits 34] [--out f.json] [--lib other.so]
 
 The server sizes jobs from this: a job of about 0.3 s is within 1% of the
 asymptotic rate."""
@@ -57,13 +57,15 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--min-s", type=float, default=1.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--lib", default=None, help="another build of the library (an A/B)")
     a = ap.parse_args()
     bits = list(range(a.min_bits, a.max_bits + 1))
-    res = {"msg": MSG.decode(), "lower": LO, "note": __doc__.split("\n\n")[0]}
-    with Context(devices=[0]) as c:
+    res = {"msg": MSG.decode(), "lower": LO, "note": __doc__.split("\n\n")[0], "lib": a.lib or "libbtcminer.so"}
+    kw = {"lib_path": os.path.abspath(a.lib)} if a.lib else {}
+    with Context(devices=[0], **kw) as c:
         print("== one device", flush=True)
         res["one_device"] = curve(c, bits, a.reps, a.min_s)
-    with Context(devices=[0] * a.slots) as c:
+    with Context(devices=[0] * a.slots, **kw) as c:
         print(f"== {a.slots} slots on GPU 0 (host combine)", flush=True)
         res[f"slots_{a.slots}_on_gpu0"] = curve(c, bits, a.reps, a.min_s)
         st = c.last_stats()

@@ -111,6 +111,13 @@ for phase in "$@"; do
       step ab_nbv2_tight 300 env AB_LO=1000000000000000 AB_MAXWIN=0 \
         AB_LIBS="t7=$D/libbtcminer_t7.so" python -u tools/ab_lens.py 52,60-62 5 2147483648 ;;
     callsize) step call_size 300 python -u tools/call_size.py --out "$OUT/call_size.json" ;;
+    callsize_ab)
+      # the submission pool (round 6) against the thread-per-call build, twice, alternating
+      for i in 1 2; do
+        step call_size_pool_$i 300 python -u tools/call_size.py --max-bits 30 --out "$OUT/call_size_pool_$i.json"
+        step call_size_spawn_$i 300 python -u tools/call_size.py --max-bits 30 --lib $D/libbtcminer_spawn.so \
+          --out "$OUT/call_size_spawn_$i.json"
+      done ;;
     pmc_c2)
       C=C2
       step pmc_${C}_fetch 90 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_${C}_fetch" -o f --output-format csv \
