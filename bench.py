@@ -1081,6 +1081,12 @@ def main():
         out["c4"] = c4
     if world > 1 and c4 is not None:
         out["c4_one_process"] = c4_one
+    elif n > 1 and c4 is not None:
+        # no launcher: this line IS the one-process mode, so its c4 block is
+        # the one-process C4 (the field is in every N > 1 line)
+        out["c4_one_process"] = {"same_as": "c4", "design": f"one process, {n} devices: this line's own context",
+                                 "GHs": c4["GHs"], "seconds": c4["seconds"], "result_ok": c4["result_ok"],
+                                 "combine": c4["combine"]}
     if n > 1:
         # what RCCL itself reported (ncclCommCount / UserRank / CuDevice per
         # rank or device) and whether the line measures N distinct GPUs

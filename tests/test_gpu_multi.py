@@ -244,6 +244,10 @@ def test_bench_one_process_rehearsal():
     assert c4["result_ok"] is True and c4["result"] == c4["golden"] == [16555811, 890536971553], c4
     assert len(c4["devices"]) == 2 and sum(d["nonces"] for d in c4["devices"]) == 2 ** 40, c4
     assert c4["combine"] == "host" and c4["GHs"] > 10 and c4["seconds"] > 1, c4
+    # every N > 1 line carries c4_one_process; without a launcher
+    # the line is the one-process mode itself, so the block points at its c4
+    one = out["c4_one_process"]
+    assert one["same_as"] == "c4" and one["GHs"] == c4["GHs"] and one["result_ok"] is True, one
     # the one-process line reports the start of each device's work (a host
     # thread per device) and, with no RCCL combine, why there is no RCCL block
     assert out["start_threads"] == 2 and out["start_skew_ms"] >= 0, out
