@@ -133,6 +133,9 @@ for phase in "$@"; do
         --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 2 --steps 2 --warmup 2 --rehearse-one-gpu ;;
     parity) step parity_campaign 600 python -u tools/parity_campaign.py ${PARITY_CASES:-3000} ${PARITY_SEED:-303} ;;
     lensweep) step len_sweep 600 python -u tools/len_sweep.py --max-len 130 ;;
+    lensweep_long)
+      # round 6: the padding-block layouts after K = 1, 2, 3, 7, 15 prefix blocks (padk<P, K>)
+      step len_sweep_long 300 python -u tools/len_sweep.py --lengths 109-117,173-181,237-245,493-501,1005-1013 ;;
     lensweep_pmc)
       # one search per length under SQ_INSTS_VALU (one stream, no tail split:
       # dispatch order = plan order); merge on the CPU with len_sweep.py --merge

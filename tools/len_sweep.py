@@ -22,6 +22,8 @@ The answers are not checked here (tests/test_gpu_parity.py checks every
 layout); this is a measurement.
 
     python tools/len_sweep.py [--max-len 130] [--nonces 2147483648]      timing sweep (GPU)
+    python tools/len_sweep.py --lengths 237-245,1005-1013                 the same over given lengths
+        (round 6: the folded padding-block kernels after 3..15 prefix blocks)
     python tools/len_sweep.py --pmc-pass                                  one search per L, prints each
         search's launches; run under BTCMINER_STREAMS=1 BTCMINER_TAIL=0 and
         `rocprofv3 --pmc SQ_INSTS_VALU` (GPU)
@@ -51,6 +53,17 @@ def launches_of(st):
     return [st.launch[i] for i in range(st.recorded)]
 
 
+def lengths(args):
+    """0..max_len, or the --lengths spec ("a-b,c,...")."""
+    if not args.lengths:
+        return list(range(args.max_len + 1))
+    out = []
+    for part in args.lengths.split(","):
+        a, _, b = part.partition("-")
+        out += list(range(int(a), int(b or a) + 1))
+    return out
+
+
 def sweep(args):
     from distributed_bitcoin_minter_amd import Context, _lib
     n = args.nonces
@@ -59,7 +72,7 @@ def sweep(args):
         probe.set_timing(True)
     with Context(devices=[0]) as ctx:
         ctx.set_timing(True)
-        for L in range(args.max_len + 1):
+        for L in lengths(args):
             msg = message(L)
             ctx.search(msg, LO, LO + n - 1)  # warm: the layout's code object loads on first launch
             best = None
@@ -152,6 +165,7 @@ def merge(sweep_path, pass_path, csv_path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-len", type=int, default=130)
+    ap.add_argument("--lengths", default=None, help="message lengths instead of 0..max_len, e.g. 237-245,1005-1013")
     ap.add_argument("--nonces", type=int, default=1 << 31)
     ap.add_argument("--pmc-pass", action="store_true")
     ap.add_argument("--merge", nargs=3, metavar=("SWEEP", "PASS", "CSV"))
