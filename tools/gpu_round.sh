@@ -131,6 +131,20 @@ for phase in "$@"; do
     rehearse_one)
       step rehearse2_c4_one 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 2 --steps 2 --warmup 2 --rehearse-one-gpu ;;
+    rehearse8_one)
+      # the driver's N = 8 launch shape, every rank and the one-process child's 8 slots on GPU 0
+      step rehearse8_c4_one 500 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port 29522 bench.py --gpus 8 --steps 2 --warmup 3 --rehearse-one-gpu ;;
+    pmc_c3)
+      C=C3
+      step pmc_${C}_fetch 90 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_${C}_fetch" -o f --output-format csv \
+        -- python3 tools/prof_one.py $C 2
+      step pmc_${C}_write 90 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_${C}_write" -o w --output-format csv \
+        -- python3 tools/prof_one.py $C 2
+      step pmc_${C}_sq 90 env PROF_ONE_LAUNCHES="$OUT/pmc_${C}_launches.json" rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU \
+        SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE \
+        -d "$OUT/pmc_${C}_sq" -o s --output-format csv -- python3 tools/prof_one.py $C 2
+      step pmc_summary_c3 60 python3 tools/pmc_summary.py "$OUT" "$OUT" C3 ;;
     parity) step parity_campaign 600 python -u tools/parity_campaign.py ${PARITY_CASES:-3000} ${PARITY_SEED:-303} ;;
     lensweep) step len_sweep 600 python -u tools/len_sweep.py --max-len 130 ;;
     lensweep_long)
