@@ -749,24 +749,48 @@ def c4_one_process(args, grp, n):
     shim (go/bitcoin/miner/gpu.go: bm_ctx_create(0)) and BASELINE configs[3]
     ("one miner process driving 8 x MI355X") are ONE process over N devices:
     bm_ctx_create(N), its per-device submission threads, balance, and
-    ncclCommInitAll + one grouped allgather.  So after the group's C4 step,
-    with every rank idle at a barrier, rank 0 measures C4 that way too: a
-    child process (bench.py --gpus N --config C4, no launcher: the one-process
-    mode), under a time limit of its own so that a failure or hang there
-    cannot cost the line; the ranks wait at the next barrier.  Under a
-    visibility mask that leaves rank 0 fewer than N devices the block is null
-    with the reason; with --rehearse-one-gpu the child runs N slots on GPU 0
-    (host combine; scaling_valid false)."""
-    import subprocess
-    grp.barrier()  # every rank's kernels are idle from here until the next barrier
-    blk = None
-    if grp.rank == 0:
+    ncclCommInitAll + one grouped allgather.  So once the line is complete,
+    rank 0 measures C4 that way too, in a child process (bench.py --gpus N
+    --config C4, no launcher: the one-process mode) under a time limit of its
+    own, so that a failure or a hang there cannot cost the line.  Before it
+    starts, every rank has closed its context and left the rendezvous, and
+    the other ranks have EXITED (rank 0 waits for their pids): idle processes
+    that have used a GPU still cost a process beside them on it (on a one-GPU
+    rehearsal, 8 idle ranks held the child at 31 of 55 GH/s,
+    profiles/r06/rehearse8_c4_one.json).  Called on every rank after
+    grp.close(); returns the block on rank 0 and None elsewhere (those ranks
+    then exit).  Under a visibility mask that leaves rank 0 fewer than N
+    devices the block says why it was skipped; with --rehearse-one-gpu the
+    child runs N slots on GPU 0 (host combine; scaling_valid false)."""
+    if grp.rank != 0:
+        return None
+    try:
+        return _c4_one_process_child(args, n)
+    except Exception as e:  # noqa: BLE001 -- reported in the block, never fatal to the line
+        return {"skipped": f"{type(e).__name__}: {e}"[:500]}
+
+
+def wait_exited(pids, timeout_s=60.0):
+    """Until none of `pids` is a live process (the other ranks, after they
+    left the rendezvous), or the timeout; returns the pids still alive."""
+    def running(pid):
         try:
-            blk = _c4_one_process_child(args, n)
-        except Exception as e:  # noqa: BLE001 -- reported in the block, never fatal to the line
-            blk = {"skipped": f"{type(e).__name__}: {e}"[:500]}
-    grp.barrier()
-    return blk
+            os.kill(pid, 0)
+        except (ProcessLookupError, PermissionError):  # gone (or a recycled pid that is not ours)
+            return False
+        try:  # an exited rank its launcher has not reaped yet is a zombie: its GPU is released
+            with open(f"/proc/{pid}/stat") as f:
+                return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+        except (OSError, IndexError):
+            return True
+
+    deadline = time.monotonic() + timeout_s
+    alive = list(pids)
+    while alive and time.monotonic() < deadline:
+        alive = [pid for pid in alive if running(pid)]
+        if alive:
+            time.sleep(0.02)
+    return alive
 
 
 def _c4_one_process_child(args, n):
@@ -1035,7 +1059,6 @@ def main():
     c4 = None if (args.no_c4 or args.config == "C4") else c4_block(args, ctx, grp, search, n)
     # the same C4 search through ONE process over the N devices
     # (the Go shim's design), measured by rank 0 while the ranks idle
-    c4_one = c4_one_process(args, grp, n) if (world > 1 and c4 is not None) else None
 
     total = hi - lo + 1
     value = total * args.steps / dt / 1e9
@@ -1079,9 +1102,7 @@ def main():
     }
     if c4 is not None:
         out["c4"] = c4
-    if world > 1 and c4 is not None:
-        out["c4_one_process"] = c4_one
-    elif n > 1 and c4 is not None:
+    if n > 1 and world == 1 and c4 is not None:
         # no launcher: this line IS the one-process mode, so its c4 block is
         # the one-process C4 (the field is in every N > 1 line)
         out["c4_one_process"] = {"same_as": "c4", "design": f"one process, {n} devices: this line's own context",
@@ -1224,10 +1245,23 @@ def main():
         out["rehearsal"] = "every rank / device is GPU 0: checks the multi-GPU split and combine, not a measurement"
     if grp.rank == 0 and n == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
+    ctx.close()
+    if world > 1 and c4 is not None:
+        # the same C4 search through ONE process over the N
+        # devices (the Go shim's design), measured by rank 0 once every other
+        # rank has left and exited
+        pids = grp.gather(os.getpid())
+        grp.close()
+        if grp.rank == 0:
+            alive = wait_exited(pids[1:])
+            blk = c4_one_process(args, grp, n)
+            if alive and blk is not None:
+                blk["ranks_still_alive"] = alive
+            out["c4_one_process"] = blk
+    else:
+        grp.close()
     if grp.rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
-    grp.close()
     if out["result_ok"] is False:
         log(f"error: result {out['result']} != golden {want}")
         sys.exit(1)

@@ -440,3 +440,19 @@ def test_pmc_same_kernel_code_hash():
     probe = os.path.join(ROOT, "distributed_bitcoin_minter_amd", "libbtcminer_probe.so")
     if os.path.exists(probe):
         assert codeobj.kernel_code_sha(probe, 18, 1) not in (None, c2)
+
+
+def test_wait_exited():
+    """bench.wait_exited: rank 0 waits for the other ranks' processes to end
+    before the one-process child opens their GPUs; it returns the pids still
+    alive at its timeout."""
+    import subprocess
+    p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(0.3)"])
+    q = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"])
+    try:
+        assert bench.wait_exited([p.pid], timeout_s=20) == []
+        p.wait()
+        assert bench.wait_exited([q.pid], timeout_s=0.2) == [q.pid]
+    finally:
+        q.kill()
+        q.wait()
