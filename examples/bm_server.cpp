@@ -96,13 +96,13 @@ constexpr size_t kRateSamples = 5;
 
 // server.py chunk_for: the multiple k >= 1 of `base` for a miner's next job.
 uint64_t chunk_for(uint64_t base, double target_s, uint64_t max_mult, double rate, uint64_t prev_mult,
-                   uint64_t remaining, double share) {
+                   double remaining, double share) {
     if (target_s <= 0 || rate <= 0) return 1;
     const double want = std::floor(rate * target_s / (double)base + 0.5);
     uint64_t k = want >= (double)max_mult ? max_mult : (uint64_t)std::max(1.0, want);
     k = std::max<uint64_t>(1, std::min({k, max_mult, 2 * std::max<uint64_t>(1, prev_mult)}));
     if (share > 0 && share < 1) {
-        const double mine = std::floor((double)remaining * share);
+        const double mine = std::floor(remaining * share);
         const uint64_t cap = (uint64_t)std::ceil(mine / (double)base);
         k = std::min(k, std::max<uint64_t>(1, cap));
     }
@@ -242,7 +242,8 @@ class BitcoinServer {
                     ++nk;
                 }
             for (const auto& kv : rates_) total += kv.second.rate() > 0 ? kv.second.rate() : known / (double)nk;
-            const uint64_t remaining = r.done ? 0 : r.upper - r.next_lower + 1;  // wraps only for all 2^64
+            // as a double: the whole 2^64 range does not fit a u64 count
+            const double remaining = r.done ? 0.0 : (double)(r.upper - r.next_lower) + 1.0;
             k = chunk_for(chunk_, target_s_, max_mult_, rate, mr.mult, remaining, total > 0 ? rate / total : 1.0);
         }
         mr.mult = k;
