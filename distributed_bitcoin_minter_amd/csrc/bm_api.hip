@@ -35,7 +35,7 @@ namespace bm {
 // search kernel table [nbv-1][P], filled by bm_inst.hip at load time; rows
 // 2 + K hold the padding-block layouts (P >= 55) with their constants folded
 // after K whole prefix blocks: search_kernel_padc<P> (K = 0, a one-block
-// message) and search_kernel_padk<P, K> (K = 1, 2)
+// message) and search_kernel_padk<P, K> (K = 1..kMaxPadPrefixBlocks = 15)
 constexpr int kSearchRows = 3 + kMaxPadPrefixBlocks;
 static const void* g_search[kSearchRows][64];
 

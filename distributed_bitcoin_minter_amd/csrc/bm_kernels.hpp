@@ -600,8 +600,8 @@ __global__ __launch_bounds__(kBlock) BM_KATTR void search_kernel_padc(
     search_body<P, 1, 0>(A, part, counter);
 }
 
-// The same after K = 1 or 2 whole prefix blocks (messages whose "msg nonce"
-// ends at byte 64K + P, P >= 55: L + D between about 119 and 191): the
+// The same after K = 1..15 whole prefix blocks (messages whose "msg nonce"
+// ends at byte 64K + P, P >= 55: L + D between about 119 and 1,023): the
 // midstate comes from kernargs, the padding block's K + W are literals
 // (W15 = 8 * (64K + P + 1)), so the 64 kernarg words the generic kernel
 // keeps in SGPRs -- more than the file holds at this occupancy, hence its

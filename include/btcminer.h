@@ -172,7 +172,7 @@ typedef struct bm_launch_stat {
     int32_t pad_block;    /* 1 when a constant padding block follows (the generic kernel: its
                              K + W from kernargs); 2 + K: the same, run by a kernel with that
                              block's constants folded in, after K whole prefix blocks (2: a
-                             one-block message, search_kernel_padc; 3, 4: K = 1, 2,
+                             one-block message, search_kernel_padc; 3..17: K = 1..15,
                              search_kernel_padk, whose entering state is the midstate) */
     int32_t digits;       /* decimal digits of every nonce in the launch */
     int32_t inner_digits; /* digits iterated by each thread's inner loop */
