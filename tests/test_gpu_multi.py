@@ -166,12 +166,17 @@ def test_reduce_empty(gpu_ctx):
     assert gpu_ctx.reduce([]) == (U64, U64)
 
 
+@pytest.mark.parametrize("slots", [1, 4])
 @pytest.mark.parametrize("fault", [0, 1, 3, 9])
-def test_failure_midway_leaves_context_usable(fault):
+def test_failure_midway_leaves_context_usable(fault, slots):
     """A search that fails after `fault` launches (some already running on the
     aux stream) returns BM_EINTERNAL, drains, and the same context then
-    answers C2 and a small window correctly."""
-    with Context(devices=[0]) as c:
+    answers C2 and a small window correctly.  With 4 slots (round 6) the
+    devices' work is submitted by the context's persistent submission threads
+    at once, so the failing launch may be any slot's: the call still fails as
+    a whole, every slot's streams are drained, and the threads serve the next
+    calls."""
+    with Context(devices=[0] * slots) as c:
         c.set_test_fault(fault)
         with pytest.raises(BtcMinerError) as ei:
             c.search(bytes.fromhex(C2["msg_hex"]), C2["lower"], C2["upper"])
