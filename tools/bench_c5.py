@@ -4,6 +4,7 @@ lspnet 10% packet drop (read and write, every endpoint).
 
     python tools/bench_c5.py [--max-nonce-bits 34] [--chunk-bits 32] [--miners 4]
                              [--clients 16] [--drop 10] [--epoch-ms 50] [--depth 2] [--window 1]
+                             [--slots 1] [--target-ms 300]
 
 Client i asks for msg "client-%02d" over [0, 2^bits - 1].  The server cuts
 every request into 2^chunk_bits-nonce jobs and spreads them
@@ -14,6 +15,13 @@ the first request to the last answer, the same figure for the bare library
 on the same GPUs, and the checks: every answer re-hashes to itself
 (bm_hash_gpu), two clients' answers equal one whole-range bm_search_gpu call,
 and every answer equals the full CPU scan in tests/golden/c5_clients.json.
+
+--slots S makes each miner one context over S device slots (round 6: a
+miner that drives several GPUs, as the Go shim's bm_ctx_create(0) does; on a
+one-GPU box the S slots share GPU 0, so each call pays S pieces' fixed costs
+on one GPU), and --target-ms is the server's per-miner job sizing
+(server.chunk_for; 0 = every job one --chunk): the pair measures what
+rate-sized jobs buy such a miner end to end.
 """
 import argparse
 import json
@@ -40,16 +48,18 @@ def main():
     ap.add_argument("--epoch-limit", type=int, default=100)
     ap.add_argument("--depth", type=int, default=2, help="jobs queued per miner (server.DEFAULT_DEPTH)")
     ap.add_argument("--window", type=int, default=1, help="LSP WindowSize (params.go default 1)")
+    ap.add_argument("--slots", type=int, default=1, help="device slots per miner (a multi-GPU miner's context)")
+    ap.add_argument("--target-ms", type=int, default=300, help="server job sizing target (0: fixed chunks)")
     a = ap.parse_args()
 
     ndev = max(1, device_count())
     p = lsp.Params(EpochLimit=a.epoch_limit, EpochMillis=a.epoch_ms, WindowSize=a.window)
     lspnet.seed(0x5EED)
     srv = lsp.NewServer(0, p)
-    bs = BitcoinServer(srv, chunk=1 << a.chunk_bits, depth=a.depth)
+    bs = BitcoinServer(srv, chunk=1 << a.chunk_bits, depth=a.depth, target_ms=a.target_ms)
     hostport = f"127.0.0.1:{srv.port}"
     threads = [threading.Thread(target=bs.serve, daemon=True)]
-    gminers = [Miner(devices=[i % ndev]) for i in range(a.miners)]
+    gminers = [Miner(devices=[i % ndev] * a.slots) for i in range(a.miners)]
     for m in gminers:
         m.search("warmup", 0, 1 << 20)  # code objects loaded before the clock starts
         threads.append(threading.Thread(target=miner.run, args=(hostport, p), kwargs={"searcher": m}, daemon=True))
@@ -82,7 +92,8 @@ def main():
 
     total = a.clients * (top + 1)
     out = {"config": "C5", "clients": a.clients, "miners": a.miners, "gpus": ndev, "drop_pct": a.drop,
-           "epoch_ms": a.epoch_ms, "window": a.window, "depth": a.depth, "max_nonce": top, "chunk": 1 << a.chunk_bits, "seconds": round(wall, 3),
+           "epoch_ms": a.epoch_ms, "window": a.window, "depth": a.depth, "max_nonce": top, "chunk": 1 << a.chunk_bits,
+           "slots_per_miner": a.slots, "target_ms": a.target_ms, "seconds": round(wall, 3),
            "GHs": round(total / wall / 1e9, 3), "server_stats": stats,
            "all_answered": all(got.get(i) is not None for i in range(a.clients))}
     with Context(devices=list(range(min(ndev, a.miners)))) as ctx:

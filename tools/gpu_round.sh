@@ -85,6 +85,15 @@ for phase in "$@"; do
     c5)
       step c5_native 300 python -u tools/bench_c5_native.py
       step c5_python 300 python -u tools/bench_c5.py ;;
+    c5_sizing)
+      # round 6: one miner driving 8 device slots (GPU 0 eight times), fixed 2^32 jobs against
+      # rate-sized ones, alternating twice; then 4 one-slot miners the same way
+      for i in 1 2; do
+        for t in 0 300; do
+          step c5_8slot_t${t}_$i 300 python -u tools/bench_c5.py --miners 1 --slots 8 --target-ms $t
+        done
+      done
+      for t in 0 300; do step c5_4miners_t$t 300 python -u tools/bench_c5.py --target-ms $t; done ;;
     prof)
       step prof_C2 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_C2" -o run --output-format csv -- $BENCH --steps 5 --warmup 2
       step prof_C2_1stream 300 env BTCMINER_STREAMS=1 rocprofv3 --kernel-trace --stats -d "$OUT/prof_C2_1stream" -o run \
