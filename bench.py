@@ -785,11 +785,10 @@ def wait_exited(pids, timeout_s=60.0):
             return True
 
     deadline = time.monotonic() + timeout_s
-    alive = list(pids)
+    alive = [pid for pid in pids if running(pid)]  # checked at least once, whatever the timeout
     while alive and time.monotonic() < deadline:
+        time.sleep(0.02)
         alive = [pid for pid in alive if running(pid)]
-        if alive:
-            time.sleep(0.02)
     return alive
 
 

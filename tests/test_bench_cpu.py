@@ -456,3 +456,100 @@ def test_wait_exited():
     finally:
         q.kill()
         q.wait()
+
+
+# bench.main() itself at world 2 on CPU (VERDICT r5 item 1's sequence): the
+# library's Context is a stand-in whose search is the oracle's scan of a small
+# range (the group combine stands in with the whole range), the workload and
+# the C4 step are shrunk, and the one-process child is replaced by a probe
+# that records whether the other ranks are still running when it starts.
+_MAIN_WORLD2 = r"""
+import json, os, sys, types
+root = sys.argv[1]
+sys.path[:0] = [root, os.path.join(root, "tests")]
+import bench
+from conftest import Oracle
+from distributed_bitcoin_minter_amd import _lib
+from distributed_bitcoin_minter_amd.dist import rank_piece
+oracle = Oracle(os.path.join(root, "oracle", "liboracle.so"))
+LO, HI = 0, 199_999
+
+def launch(n):
+    return types.SimpleNamespace(p=18, nbv=1, pad_block=0, digits=10, inner_digits=2, nonces=n, grid=1792,
+                                 tasks_per_thread=1, ms=20.0, clock_ghz=0.0, device=0)
+
+class FakeCtx:
+    def __init__(self, devices=None, rank=None, world=None, **kw):
+        self.rank_, self.world_, self._joined, self.shares, self.piece = rank, world, False, None, None
+    def join(self, uid, timeout_ms=0): self._joined = True
+    def joined(self): return self._joined
+    def leave(self): self._joined = False
+    def set_peer_timeout(self, ms): pass
+    def set_timing(self, on): pass
+    def num_devices(self): return 1
+    def set_split(self, s): self.shares = s
+    def close(self): pass
+    def search(self, msg, lo, hi):
+        self.piece = rank_piece(lo, hi, self.rank_, self.world_, self.shares)
+        return oracle.search(msg, lo, hi)   # the in-library allgather: the whole range's answer
+    def last_stats(self):
+        n = 1 << 31  # as a 2^31-nonce piece would report: the warmup rates are measured on it
+        L = launch(n)
+        return types.SimpleNamespace(
+            nonces=n, span_ms=40.0 + 2 * self.rank_, combine_used=_lib.BM_COMBINED_RCCL, rccl_status=0,
+            rccl_nranks=self.world_, rccl_rank=self.rank_, devices=1, dev_nonces=[n], dev_span_ms=[40.0],
+            dev_rccl_rank=[self.rank_], dev_rccl_device=[self.rank_], rccl_version=22703, rccl_init_ms=40.0,
+            rccl_allgather_ms=0.05, combine_ms=0.2, start_threads=1, dev_start_ms=[0.0], dev_allgather_ms=[0.05],
+            launches=1, recorded=1, launch=[L])
+
+rank = int(os.environ["RANK"])
+open(os.path.join(os.environ["PIDDIR"], f"pid.{rank}"), "w").write(str(os.getpid()))
+bench.Context = FakeCtx
+_lib.load = lambda: None
+bench.device_count = lambda: 2
+bench.rccl_unique_id = lambda: os.urandom(128)
+bench.device_pci_bus_id = lambda d: "0000:%02x:00.0" % (0x10 + d)
+bench.measure_clock = lambda *a, **k: None
+_wl = bench.workload
+bench.workload = lambda cfg, n: (b"bradfitz", LO, HI, "weak", "C2 (shrunk for a CPU test)") if cfg == "C2" else _wl(cfg, n)
+bench.golden = lambda msg, lo, hi: list(oracle.search(msg, lo, hi)) if hi < 10 ** 6 else None
+bench.c4_block = lambda args, ctx, grp, search, n: {"GHs": 1.0, "seconds": 1.0, "result": [0, 0], "golden": None,
+                                                  "result_ok": None, "combine": "rccl"}
+
+def probe_child(args, n):
+    others = [int(open(os.path.join(os.environ["PIDDIR"], f"pid.{r}")).read()) for r in range(1, 2)]
+    return {"GHs": 2.0, "others_running": bench.wait_exited(others, timeout_s=0.0), "n": n}
+bench._c4_one_process_child = probe_child
+sys.argv = ["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "3", "--no-cpu-baseline", "--clock-sample", "0"]
+bench.main()
+"""
+
+
+def test_bench_main_world2_one_process_after_ranks_exit(oracle, tmp_path):
+    """bench.main() at world 2 over the file rendezvous, on CPU: the line
+    carries the median-of-steps calibration (two warm steps per rank), the
+    RCCL block and the ranks; rank 1 exits before rank 0 runs the one-process
+    C4 child (the probe sees no other rank running), and only rank 0 prints."""
+    import json
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE="2", PIDDIR=str(tmp_path))
+        procs.append(subprocess.Popen([sys.executable, "-c", _MAIN_WORLD2, ROOT], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=180) + (p.returncode,) for p in procs]
+    assert [rc for _, _, rc in outs] == [0, 0], [e[-2000:] for _, e, _ in outs]
+    assert outs[1][0].strip() == ""  # only rank 0 prints the line
+    line = json.loads(outs[0][0].strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["result_ok"] is True and line["result"] == list(oracle.search(b"bradfitz", 0, 199_999))
+    sp = line["config"]["split"]
+    assert sp["mode"] == "measured rank rates, median of warmup steps 2..3" and len(sp["step_rates_nonces_per_ms"][0]) == 2
+    assert sp["shares"][0] == 65536 and sp["shares"][1] < 65536  # rank 1 reported the longer span
+    assert line["rccl"]["version_str"] == "2.27.3" and line["scaling_valid"] is True
+    one = line["c4_one_process"]
+    assert one["GHs"] == 2.0 and one["n"] == 2 and one["others_running"] == [], one
