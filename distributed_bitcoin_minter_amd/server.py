@@ -51,7 +51,8 @@ and at most the miner's rate-proportional share of what the request has left
 miners idle).  The rate is the median of the miner's last 5 jobs, each its
 nonces over the time from when the miner could start it (its send, or the
 previous result if that came later) to its result.  A new miner gets one
-base.  ``target_ms = 0`` keeps the fixed chunk.  The wire format is
+base, and a lost miner's chunk is re-issued cut to the size of whoever takes
+it.  ``target_ms = 0`` keeps the fixed chunk.  The wire format is
 unchanged: a Request's [Lower, Upper] is just wider.
 
 Job queue depth.  Each miner holds up to ``depth`` jobs (default 2; the
@@ -122,9 +123,16 @@ class _Request:
         return not self.has_work() and self.inflight == 0
 
     def take(self, chunk):
-        """Next chunk [lo, hi] (inclusive)."""
+        """Next chunk [lo, hi] (inclusive), at most `chunk` nonces.  A lost
+        miner's chunk is re-issued first, cut to the taker's size (a fast
+        miner's big job does not land whole on a slow one); its rest stays at
+        the front of the queue."""
         if self.retry:
-            return self.retry.popleft()
+            lo, hi = self.retry.popleft()
+            if hi - lo >= chunk:  # more than `chunk` nonces: the rest goes back first
+                self.retry.appendleft((lo + chunk, hi))
+                hi = lo + chunk - 1
+            return lo, hi
         lo = self.next_lower
         hi = lo + chunk - 1 if self.upper - lo >= chunk else self.upper
         if hi == self.upper:
@@ -294,7 +302,7 @@ class BitcoinServer:
             r = self._pick()
             if r is None:
                 return
-            lo, hi = r.take(self.chunk if r.retry else self.chunk_size(mid, r))
+            lo, hi = r.take(self.chunk_size(mid, r))
             try:
                 self.srv.Write(mid, NewRequest(r.data, lo, hi).marshal())
             except lsp.LSPError:

@@ -56,10 +56,16 @@ struct Request {
         : rid(id), client(c), data(m.Data), upper(m.Upper), next_lower(m.Lower), done(m.Lower > m.Upper) {}
     bool has_work() const { return !retry.empty() || !done; }
     bool finished() const { return !has_work() && inflight == 0; }
+    // At most `chunk` nonces; a lost miner's chunk first, cut to the taker's
+    // size (server.py _Request.take), its rest left at the front.
     Range take(uint64_t chunk) {
         if (!retry.empty()) {
-            const Range r = retry.front();
+            Range r = retry.front();
             retry.pop_front();
+            if (r.second - r.first >= chunk) {
+                retry.push_front({r.first + chunk, r.second});
+                r.second = r.first + chunk - 1;
+            }
             return r;
         }
         const uint64_t lo = next_lower;
@@ -256,7 +262,7 @@ class BitcoinServer {
             if (!mid) return;
             Request* r = pick();
             if (!r) return;
-            const Range c = r->take(r->retry.empty() ? chunk_size(mid, *r) : chunk_);
+            const Range c = r->take(chunk_size(mid, *r));
             try {
                 srv_.Write(mid, bitcoin::NewRequest(r->data, c.first, c.second).Marshal());
             } catch (const lsp::LSPError&) {  // miner already gone (server.go:177-179)

@@ -584,3 +584,27 @@ def test_rate_sized_chunks_end_to_end(oracle):
     ratio = med(fast.jobs) / med(slow.jobs)
     assert 4.0 <= ratio <= 12.0, (fast.jobs, slow.jobs)
     s.close()
+
+
+def test_lost_fast_miners_chunk_is_cut_for_the_slow_one():
+    """A fast miner holding rate-sized jobs dies: its chunks go back to the
+    front of the request and are re-issued cut to the size of the miner that
+    takes them (here a new miner: one base), in ascending order, the rest
+    staying queued; the request still tiles exactly."""
+    now = [0.0]
+    f, s = make(1000, depth=2, target_ms=200, clock=lambda: now[0])
+    s._on_message(1, NewJoin())
+    s._on_message(100, NewRequest("x", 0, 10 ** 7 - 1))
+    for _ in range(6):  # miner 1 runs at 160k nonces/s: its jobs ramp up to 32 bases
+        rid, lo, hi, sent = s.miners[1][0]
+        now[0] = max(now[0], sent) + (hi - lo + 1) / 160_000
+        s._on_message(1, NewResult(lo, lo))
+    big = [b - a + 1 for a, b in f.jobs_for(1)]
+    assert big[-1] >= 8000, big
+    held = [(lo, hi) for _, lo, hi, _ in s.miners[1]]
+    s._on_lost(1)
+    s._on_message(2, NewJoin())  # a new miner: no rate yet, one base per job
+    got = f.jobs_for(2)
+    assert got[0] == (held[0][0], held[0][0] + 999) and got[1] == (held[0][0] + 1000, held[0][0] + 1999), (got, held)
+    r = list(s.requests.values())[0]
+    assert r.retry[0] == (held[0][0] + 2000, held[0][1]) and r.retry[1] == held[1]
