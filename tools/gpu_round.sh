@@ -122,6 +122,8 @@ for phase in "$@"; do
     callsize) step call_size 300 python -u tools/call_size.py --out "$OUT/call_size.json" ;;
     callsize_ab)
       # the submission pool (round 6) against the thread-per-call build, twice, alternating
+      # ($D/libbtcminer_spawn.so: the library built from commit 95a42c3, before the pool;
+      # profiles/r06/call_size_ab/ holds the result)
       for i in 1 2; do
         step call_size_pool_$i 300 python -u tools/call_size.py --max-bits 30 --out "$OUT/call_size_pool_$i.json"
         step call_size_spawn_$i 300 python -u tools/call_size.py --max-bits 30 --lib $D/libbtcminer_spawn.so \
